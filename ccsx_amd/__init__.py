@@ -1,0 +1,10 @@
+"""ccsx_amd -- MI355X-native engine for ccsx's per-ZMW circular-consensus hot path.
+
+See DESIGN.md.  The product is the in-tree ``libccsx_amd.so`` (HIP kernels for
+gfx950 + C-ABI, include/*.h); this package holds its build script and ctypes
+bindings.
+"""
+from .native import (MODE_PRIMITIVE, MODE_SHRED, Engine, GpuError, Prepared, lib, pairwise, prepare,  # noqa: F401
+                     prepare_segments, read_zmws, revcomp, synth_zmw)
+
+__version__ = "0.1.0"

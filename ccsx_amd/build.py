@@ -1,0 +1,126 @@
+"""Build the in-tree native libraries.
+
+* ``ccsx_amd/libccsx_amd.so`` -- the product: the gfx950 HIP kernel, its
+  batched C-ABI (include/ccsx_gpu.h), the bspoa-compatible API
+  (include/ccsx_bspoa.h) and the host preparation code (include/ccsx_host.h).
+  Compiled with ``hipcc --offload-arch=gfx950``; works without a GPU present.
+* ``ccsx_amd/bin/ccsx`` -- the C host program (ccsx's CLI, main.c:723-870).
+* ``oracle/liboracle.so`` -- the CPU restatement used as the checker by the
+  tests and bench.py's cpu_baseline leg (test infrastructure, not shipped).
+
+Incremental: a target is rebuilt only when one of its sources is newer.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+INC = os.path.join(ROOT, "include")
+OBJ = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(HERE, "libccsx_amd.so")
+BIN = os.path.join(HERE, "bin", "ccsx")
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+ARCH = os.environ.get("CCSX_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc"), shutil.which("hipcc") or ""):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm required to build ccsx_amd)")
+
+
+def _rocm_inc() -> str:
+    return os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "include")
+
+
+def _stale(target: str, sources: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _headers() -> list[str]:
+    hs = []
+    for d in (INC, CSRC, os.path.join(CSRC, "host")):
+        for f in os.listdir(d):
+            if f.endswith(".h"):
+                hs.append(os.path.join(d, f))
+    return hs
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout)
+        raise RuntimeError("build failed: " + " ".join(cmd))
+
+
+def build_product(verbose: bool = False) -> str:
+    hipcc = _hipcc()
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = _headers()
+    srcs = [
+        os.path.join(CSRC, "ccsx_kernel.hip"),
+        os.path.join(CSRC, "ccsx_gpu.cpp"),
+        os.path.join(CSRC, "bspoa_gpu.cpp"),
+        os.path.join(CSRC, "host", "prepare.cpp"),
+        os.path.join(CSRC, "host", "pairwise.cpp"),
+        os.path.join(CSRC, "host", "seqio.cpp"),
+    ]
+    common = ["-O3", "-std=c++17", "-fPIC", "-I" + INC, "-I" + CSRC, "-I" + os.path.join(CSRC, "host")]
+    objs = []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        objs.append(o)
+        if _stale(o, [s] + hdrs):
+            if s.endswith(".hip"):
+                cmd = [hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + ["-c", s, "-o", o]
+            else:
+                cmd = [hipcc, "-x", "c++"] + common + ["-D__HIP_PLATFORM_AMD__", "-I" + _rocm_inc(), "-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd))
+            _run(cmd)
+    if _stale(LIB, objs):
+        cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lpthread"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+    # the C host program
+    main_src = os.path.join(CSRC, "host", "main.cpp")
+    if os.path.exists(main_src) and _stale(BIN, [main_src, LIB] + hdrs):
+        os.makedirs(os.path.dirname(BIN), exist_ok=True)
+        cmd = [hipcc, "-x", "c++"] + common + ["-D__HIP_PLATFORM_AMD__", "-I" + _rocm_inc(), main_src, "-o", BIN,
+                                               "-L" + HERE, "-lccsx_amd", "-Wl,-rpath,$ORIGIN/..", "-lz", "-lpthread"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+    return LIB
+
+
+def build_oracle(verbose: bool = False) -> str:
+    srcs = [os.path.join(ORACLE_DIR, f) for f in sorted(os.listdir(ORACLE_DIR)) if f.endswith(".c")]
+    hdrs = [os.path.join(ORACLE_DIR, f) for f in os.listdir(ORACLE_DIR) if f.endswith(".h")]
+    if _stale(ORACLE_LIB, srcs + hdrs):
+        cmd = ["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-o", ORACLE_LIB] + srcs + ["-lpthread", "-lz"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+    return ORACLE_LIB
+
+
+def build_all(verbose: bool = False) -> None:
+    build_product(verbose)
+    build_oracle(verbose)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True)

@@ -1,0 +1,346 @@
+// ccsx_gpu.cpp -- host side of the batched C-ABI (include/ccsx_gpu.h).
+//
+// Stages a chunk of ZMWs into HBM (one sequence arena, segment tables, one
+// descriptor and one workspace slab per ZMW, laid out by ccsx_layout.h),
+// launches one 64-lane workgroup per ZMW and copies the CCS strings back.
+// This is the device boundary that replaces kt_for(ccs_for2/ccs_for) in step 1
+// of ccsx's pipeline (main.c:698-706).
+#include "ccsx_gpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ccsx_layout.h"
+
+extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = std::max<size_t>(n, 256);
+        hipError_t e = hipMalloc(&p, c);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const
+    {
+        return static_cast<T *>(p);
+    }
+};
+
+}  // namespace
+
+struct ccsx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    // staged batch
+    size_t nz = 0;
+    uint32_t lds_read_words = 0, lds_nmax = 0;
+    uint64_t seq_bytes = 0, ws_bytes = 0, out_bytes = 0, msa_bytes = 0;
+    uint32_t nseg_total = 0;
+    std::vector<ccsx::ZmwDesc> desc;
+    DevBuf d_seq, d_soff, d_slen, d_desc, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
+    // fetched results
+    std::vector<uint8_t> h_out;
+    std::vector<uint32_t> h_olen, h_ncols;
+    std::vector<int32_t> h_status;
+    std::vector<unsigned long long> h_cells;
+    std::vector<uint8_t> h_msa;
+};
+
+static int fail(ccsx_ctx *c, const char *what, hipError_t e)
+{
+    if (c) {
+        c->err = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return -1;
+}
+
+#define HIPCHK(c, call)                                   \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return fail((c), #call, e_); \
+    } while (0)
+
+extern "C" {
+
+int ccsx_gpu_open(int device, ccsx_ctx **out)
+{
+    *out = nullptr;
+    auto *c = new ccsx_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e != hipSuccess) {
+        fprintf(stderr, "[ccsx_gpu] cannot open device %d: %s\n", device, hipGetErrorString(e));
+        delete c;
+        return -1;
+    }
+    *out = c;
+    return 0;
+}
+
+void ccsx_gpu_close(ccsx_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    DevBuf *bufs[] = {&c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_ws, &c->d_out,
+                      &c->d_msa, &c->d_olen, &c->d_ncols, &c->d_status, &c->d_cells};
+    for (DevBuf *b : bufs) b->release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *ccsx_gpu_error(const ccsx_ctx *c) { return c ? c->err.c_str() : "no context"; }
+
+const char *ccsx_gpu_status_str(int32_t s)
+{
+    switch (s) {
+    case ccsx::kOk: return "ok";
+    case ccsx::kErrRows: return "graph rows exceed capacity";
+    case ccsx::kErrEdges: return "graph edges exceed capacity";
+    case ccsx::kErrMulti: return "multi-predecessor rows exceed capacity";
+    case ccsx::kErrSpill: return "spilled DP rows exceed capacity";
+    case ccsx::kErrInDegree: return "node in-degree > 255";
+    case ccsx::kErrReadLen: return "read longer than the LDS read buffer";
+    case ccsx::kErrOut: return "consensus longer than the output slab";
+    case ccsx::kErrTrace: return "traceback did not terminate";
+    default: return "unknown status";
+    }
+}
+
+// internal: stage with an optional MSA slab per ZMW (single-POA mode)
+int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa)
+{
+    if (!c) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    c->nz = nz;
+    c->desc.assign(nz, ccsx::ZmwDesc{});
+    uint64_t seq_b = 0, ws_b = 0, out_b = 0, msa_b = 0;
+    uint32_t nseg = 0, lmax_all = 0, nmax = 0;
+    for (size_t i = 0; i < nz; ++i) {
+        const ccsx_zmw_in &zi = z[i];
+        uint64_t S = 0, hi = 0;
+        uint32_t lmax = 0;
+        for (uint32_t k = 0; k < zi.nseg; ++k) {
+            S += zi.seg_len[k];
+            lmax = std::max(lmax, zi.seg_len[k]);
+            hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
+        }
+        if (S + zi.nseg + 64 > 0x3FFFFFFFull) {
+            c->err = "ZMW too large (sum of segment lengths >= 2^30)";
+            return -1;
+        }
+        ccsx::ZmwDesc &d = c->desc[i];
+        ccsx::zcaps(d, S, lmax, zi.nseg);
+        d.seg0 = nseg;
+        d.seq_off = seq_b;
+        seq_b += hi;
+        ccsx::ZLayout L;
+        ccsx::zlayout(L, d);
+        d.ws_off = ws_b;
+        ws_b = ccsx::align256(ws_b + L.total);
+        d.out_off = out_b;
+        out_b += d.outcap;
+        d.msa_off = msa_b;
+        d.msacap = with_msa ? uint32_t((S + 16) * (zi.nseg + 4)) : 0u;
+        msa_b += d.msacap;
+        nseg += zi.nseg;
+        lmax_all = std::max(lmax_all, lmax);
+        nmax = std::max(nmax, zi.nseg);
+    }
+    c->seq_bytes = seq_b, c->ws_bytes = ws_b, c->out_bytes = out_b, c->msa_bytes = msa_b;
+    c->nseg_total = nseg;
+    c->lds_read_words = (lmax_all + 15) / 16 + 1;
+    c->lds_nmax = std::max<uint32_t>(nmax, 1);
+    size_t freeb = 0, totb = 0;
+    HIPCHK(c, hipMemGetInfo(&freeb, &totb));
+    const uint64_t need = seq_b + ws_b + out_b + msa_b + uint64_t(nseg) * 8 + nz * (sizeof(ccsx::ZmwDesc) + 32);
+    if (need + (1ull << 30) > freeb + c->d_ws.cap + c->d_seq.cap + c->d_out.cap + c->d_msa.cap) {
+        char m[160];
+        snprintf(m, sizeof m, "batch needs %.1f GB of device memory, %.1f GB free: use a smaller chunk",
+                 need / 1e9, freeb / 1e9);
+        c->err = m;
+        return -1;
+    }
+    HIPCHK(c, c->d_seq.reserve(seq_b));
+    HIPCHK(c, c->d_soff.reserve(size_t(nseg) * 4));
+    HIPCHK(c, c->d_slen.reserve(size_t(nseg) * 4));
+    HIPCHK(c, c->d_desc.reserve(nz * sizeof(ccsx::ZmwDesc)));
+    HIPCHK(c, c->d_ws.reserve(ws_b));
+    HIPCHK(c, c->d_out.reserve(out_b));
+    HIPCHK(c, c->d_msa.reserve(msa_b));
+    HIPCHK(c, c->d_olen.reserve(nz * 4));
+    HIPCHK(c, c->d_ncols.reserve(nz * 4));
+    HIPCHK(c, c->d_status.reserve(nz * 4));
+    HIPCHK(c, c->d_cells.reserve(nz * 8));
+    // host staging of the sequence arena and segment tables
+    std::vector<uint8_t> hseq(seq_b);
+    std::vector<uint32_t> hoff(nseg), hlen(nseg);
+    for (size_t i = 0; i < nz; ++i) {
+        const ccsx_zmw_in &zi = z[i];
+        const ccsx::ZmwDesc &d = c->desc[i];
+        uint64_t hi = 0;
+        for (uint32_t k = 0; k < zi.nseg; ++k) {
+            hoff[d.seg0 + k] = zi.seg_off[k];
+            hlen[d.seg0 + k] = zi.seg_len[k];
+            hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
+        }
+        if (hi) memcpy(hseq.data() + d.seq_off, zi.seqs, hi);
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_seq.p, hseq.data(), seq_b, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_soff.p, hoff.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_slen.p, hlen.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_desc.p, c->desc.data(), nz * sizeof(ccsx::ZmwDesc), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int ccsx_gpu_stage(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz) { return ccsx_gpu_stage_ex(c, z, nz, 0); }
+
+int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
+{
+    if (!c) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->nz == 0) {
+        if (kernel_ms) *kernel_ms = 0.f;
+        return 0;
+    }
+    ccsx::KArgs a{};
+    a.seq = c->d_seq.as<uint8_t>();
+    a.soff = c->d_soff.as<uint32_t>();
+    a.slen = c->d_slen.as<uint32_t>();
+    a.desc = c->d_desc.as<ccsx::ZmwDesc>();
+    a.ws = c->d_ws.as<uint8_t>();
+    a.out = c->d_out.as<uint8_t>();
+    a.msa = c->d_msa.as<uint8_t>();
+    a.out_len = c->d_olen.as<uint32_t>();
+    a.ncols = c->d_ncols.as<uint32_t>();
+    a.status = c->d_status.as<int32_t>();
+    a.cells = c->d_cells.as<unsigned long long>();
+    a.mode = mode;
+    a.nzmw = uint32_t(c->nz);
+    a.lds_read_words = c->lds_read_words;
+    a.lds_nmax = c->lds_nmax;
+    const uint32_t lds = uint32_t(ccsx::kRing * 260 * 4 + (c->lds_read_words + c->lds_nmax) * 4);
+    if (lds > 160 * 1024) {
+        c->err = "reads too long for the LDS read buffer";
+        return -1;
+    }
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, ccsx_launch_zmw(&a, lds, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (kernel_ms) *kernel_ms = ms;
+    return 0;
+}
+
+int ccsx_gpu_launch(ccsx_ctx *c, int mode, float *kernel_ms)
+{
+    if (mode != CCSX_MODE_SHRED && mode != CCSX_MODE_PRIMITIVE) {
+        if (c) c->err = "mode must be CCSX_MODE_SHRED or CCSX_MODE_PRIMITIVE";
+        return -1;
+    }
+    return ccsx_gpu_launch_ex(c, mode, kernel_ms);
+}
+
+int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
+{
+    if (!c) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t nz = c->nz;
+    c->h_out.resize(c->out_bytes);
+    c->h_olen.resize(nz);
+    c->h_status.resize(nz);
+    c->h_cells.resize(nz);
+    if (nz) {
+        HIPCHK(c, hipMemcpyAsync(c->h_olen.data(), c->d_olen.p, nz * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_status.data(), c->d_status.p, nz * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_cells.data(), c->d_cells.p, nz * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_out.data(), c->d_out.p, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    int bad = 0;
+    for (size_t i = 0; i < nz; ++i) {
+        out[i].ccs = reinterpret_cast<const char *>(c->h_out.data() + c->desc[i].out_off);
+        out[i].len = c->h_status[i] ? 0 : c->h_olen[i];
+        out[i].status = c->h_status[i];
+        out[i].cells = c->h_cells[i];
+        if (c->h_status[i] && !bad) {
+            bad = 1;
+            char m[200];
+            snprintf(m, sizeof m, "ZMW %zu of the batch failed on the device: %s", i,
+                     ccsx_gpu_status_str(c->h_status[i]));
+            c->err = m;
+        }
+    }
+    return bad ? -2 : 0;
+}
+
+int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out)
+{
+    int r = ccsx_gpu_stage(c, z, nz);
+    if (r) return r;
+    r = ccsx_gpu_launch(c, mode, nullptr);
+    if (r) return r;
+    return ccsx_gpu_fetch(c, out);
+}
+
+uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *c)
+{
+    return c ? c->seq_bytes + c->ws_bytes + c->out_bytes + c->msa_bytes : 0;
+}
+
+// single-POA path used by the bspoa-compatible API (bspoa_gpu.cpp)
+int ccsx_gpu_single_poa(ccsx_ctx *c, const ccsx_zmw_in *z, const uint8_t **cns, uint32_t *ncns,
+                        const uint8_t **msa, uint32_t *ncols)
+{
+    int r = ccsx_gpu_stage_ex(c, z, 1, 1);
+    if (r) return r;
+    r = ccsx_gpu_launch_ex(c, ccsx::kSinglePoa, nullptr);
+    if (r) return r;
+    ccsx_zmw_out o;
+    r = ccsx_gpu_fetch(c, &o);
+    if (r) return r;
+    c->h_ncols.resize(1);
+    HIPCHK(c, hipMemcpy(c->h_ncols.data(), c->d_ncols.p, 4, hipMemcpyDeviceToHost));
+    const uint64_t mb = uint64_t(c->h_ncols[0]) * (z->nseg + 4);
+    c->h_msa.resize(mb + 1);
+    if (mb) HIPCHK(c, hipMemcpy(c->h_msa.data(), c->d_msa.p, mb, hipMemcpyDeviceToHost));
+    *cns = reinterpret_cast<const uint8_t *>(o.ccs);
+    *ncns = o.len;
+    *msa = c->h_msa.data();
+    *ncols = c->h_ncols[0];
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,939 @@
+// ccsx_kernel.hip -- MI355X (gfx950) consensus hot path of ccsx.
+//
+// One 64-lane wavefront owns one ZMW for the whole of ccs_for2 (main.c:510-647,
+// shredded mode) or ccs_for (main.c:455-508, -P): the window loop, every
+// bspoa call (beg/push/end/tidy_msa, SPEC.md §2-§6), the breakpoint scan and
+// the CCS emission all run on the device.  The host only runs ccs_prepare and
+// hands over strand-normalised segments.
+//
+// Per DP row (one graph node, W = 128 read positions) each lane owns two
+// adjacent cells.  The in-row insertion recurrence is an exclusive prefix max
+// done with DPP row_shr / row_bcast (no LDS); the last kRing rows live in an
+// LDS ring in an even/odd split layout (conflict-free ds_read_b32 for any
+// band shift); rows needed further back are spilled to HBM.  Traceback codes
+// (4 bits/cell, plus predecessor slots for multi-predecessor nodes) stream to
+// HBM, coalesced, 64 B per row.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ccsx_layout.h"
+
+namespace ccsx {
+
+constexpr int kO = -3, kE = -2, kMs = 2, kXs = -6;  // main.c:842-847
+enum { HC_MPRED = 0, HC_MSRC = 1, HC_DEL = 2, HC_INS = 3 };
+enum : uint32_t { EV_ALN = 0u, EV_INS = 1u, EV_LEAD = 2u };
+constexpr uint32_t kNewBit = 0x80000000u;
+
+
+
+// ----------------------------------------------------------------------------
+// wave primitives (gfx9 DPP: row_shr, row_bcast15/31, wave_shr1)
+// ----------------------------------------------------------------------------
+template <int CTRL, int RM = 0xF, int BM = 0xF>
+__device__ __forceinline__ int dpp(int old, int v)
+{
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, BM, false);
+}
+
+__device__ __forceinline__ int wave_incl_max(int v)
+{
+    v = max(v, dpp<0x111>(kNeg, v));
+    v = max(v, dpp<0x112>(kNeg, v));
+    v = max(v, dpp<0x114>(kNeg, v));
+    v = max(v, dpp<0x118>(kNeg, v));
+    v = max(v, dpp<0x142, 0xA>(kNeg, v));
+    v = max(v, dpp<0x143, 0xC>(kNeg, v));
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_sum(int v)
+{
+    v += dpp<0x111>(0, v);
+    v += dpp<0x112>(0, v);
+    v += dpp<0x114>(0, v);
+    v += dpp<0x118>(0, v);
+    v += dpp<0x142, 0xA>(0, v);
+    v += dpp<0x143, 0xC>(0, v);
+    return v;
+}
+
+__device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old, v); }
+
+__device__ __forceinline__ int wave_max(int v) { return __builtin_amdgcn_readlane(wave_incl_max(v), 63); }
+
+__device__ __forceinline__ int wave_min(int v) { return -wave_max(-v); }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template <class T>
+__device__ __forceinline__ T uni(T v)
+{
+    return (T)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__device__ __forceinline__ uint32_t enc_base(uint32_t c)
+{
+    // SPEC.md §1: A/a=0 C/c=1 G/g=2 T/t/U/u=3, anything else 0
+    c |= 0x20u;
+    return c == 'c' ? 1u : c == 'g' ? 2u : (c == 't' || c == 'u') ? 3u : 0u;
+}
+
+// ----------------------------------------------------------------------------
+// per-ZMW state
+// ----------------------------------------------------------------------------
+struct Z {
+    ZmwDesc d;
+    ZLayout L;
+    uint8_t *ws;
+    const uint8_t *seq;
+    int32_t *lds;        // ring: kRing * 256 ints
+    int32_t *meta;       // kRing * 4 ints: off, rmax, rarg, tof
+    uint32_t *rd;        // packed 2-bit read codes
+    uint32_t *pos;       // shredding cursors
+    uint32_t rdcap;      // bases that fit in rd
+    int cur;
+    uint32_t R, E;
+    int32_t status;
+    unsigned long long cells;
+};
+
+template <class T>
+__device__ __forceinline__ T *P(const Z &z, uint64_t off)
+{
+    return reinterpret_cast<T *>(z.ws + off);
+}
+
+__device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return (z.rd[j >> 4] >> ((j & 15u) * 2u)) & 3u; }
+
+// ----------------------------------------------------------------------------
+// push: stage read k (ASCII in HBM) into LDS as 2-bit codes
+// ----------------------------------------------------------------------------
+__device__ void load_read(Z &z, const uint8_t *src, uint32_t m)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t nwd = (m + 15) / 16;
+    for (uint32_t w = lane; w < nwd; w += 64) {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b) {
+            const uint32_t j = w * 16 + b;
+            const uint32_t c = j < m ? enc_base(src[j]) : 0u;
+            x |= c << (2 * b);
+        }
+        z.rd[w] = x;
+    }
+    __syncthreads();
+}
+
+// ----------------------------------------------------------------------------
+// SPEC.md §3: pre-pass -- which rows must be spilled (a successor further than
+// kRing rows away reads them after their LDS slot is reused)
+// ----------------------------------------------------------------------------
+__device__ void mark_spills(Z &z)
+{
+    const uint32_t lane = threadIdx.x;
+    uint8_t *spf = P<uint8_t>(z, z.L.spf);
+    const uint32_t *poff = P<uint32_t>(z, z.L.poff[z.cur]);
+    const uint32_t *pred = P<uint32_t>(z, z.L.pred[z.cur]);
+    for (uint32_t r = lane; r < z.R; r += 64) spf[r] = 0;
+    __syncthreads();
+    for (uint32_t s = lane; s < z.R; s += 64) {
+        const uint32_t e1 = poff[s + 1];
+        for (uint32_t e = poff[s]; e < e1; ++e) {
+            const uint32_t p = pred[e];
+            if (s - p > (uint32_t)kRing) spf[p] = 1;
+        }
+    }
+    __syncthreads();
+}
+
+// read the two cells of lane l at band index 2l+c (c wave-uniform) from a row
+// stored in the even/odd split layout [Hev|Hod|Dev|Dod] x 64 ints
+template <int ARR>
+__device__ __forceinline__ int cell_lds(const int32_t *row, int c, int lane)
+{
+    const int i = 2 * lane + c;
+    if ((unsigned)i >= (unsigned)kW) return kNeg;
+    return row[(ARR + (i & 1)) * 64 + (i >> 1)];
+}
+
+template <int ARR>
+__device__ __forceinline__ int cell_glb(const int32_t *row, int c, int lane)
+{
+    const int i = 2 * lane + c;
+    if ((unsigned)i >= (unsigned)kW) return kNeg;
+    return row[(ARR + (i & 1)) * 64 + (i >> 1)];
+}
+
+struct PredRow {
+    int32_t off, rmax, rarg;
+};
+
+__device__ __forceinline__ PredRow pred_meta(const Z &z, uint32_t r, uint32_t p)
+{
+    PredRow m;
+    if (r - p <= (uint32_t)kRing) {
+        const int32_t *mt = z.meta + (p % kRing) * 4;
+        m.off = mt[0], m.rmax = mt[1], m.rarg = mt[2];
+    } else {
+        m.off = P<int32_t>(z, z.L.roff)[p];
+        m.rmax = P<int32_t>(z, z.L.rmx)[p];
+        m.rarg = P<int32_t>(z, z.L.rag)[p];
+    }
+    return m;
+}
+
+// ----------------------------------------------------------------------------
+// SPEC.md §3: banded read-vs-graph DP for one read (codes in z.rd, length m)
+// ----------------------------------------------------------------------------
+__device__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
+{
+    const int lane = threadIdx.x;
+    const uint32_t R = z.R;
+    const uint8_t *nb = P<uint8_t>(z, z.L.nb[z.cur]);
+    const uint32_t *poff = P<uint32_t>(z, z.L.poff[z.cur]);
+    const uint32_t *pred = P<uint32_t>(z, z.L.pred[z.cur]);
+    const uint8_t *spf = P<uint8_t>(z, z.L.spf);
+    int32_t *g_roff = P<int32_t>(z, z.L.roff);
+    int32_t *g_rmx = P<int32_t>(z, z.L.rmx);
+    int32_t *g_rag = P<int32_t>(z, z.L.rag);
+    uint32_t *g_tof = P<uint32_t>(z, z.L.tof);
+    uint32_t *g_sslot = P<uint32_t>(z, z.L.sslot);
+    uint8_t *trace = P<uint8_t>(z, z.L.trace);
+    int32_t *spill = P<int32_t>(z, z.L.spill);
+    const int32_t lim = m > (uint32_t)kW ? (int32_t)(m - kW) : 0;
+    const int t0 = 2 * lane, t1 = 2 * lane + 1;
+
+    int32_t bE = INT32_MIN;
+    uint32_t bR = 0, bJ = 0;
+    uint32_t nmulti = 0, nspill = 0;
+    uint32_t blk_nb = 0, blk_po = 0, blk_np = 0, blk_p0 = 0, blk_p1 = 0, blk_sp = 0;
+
+    for (uint32_t r = 0; r < R; ++r) {
+        if ((r & 63u) == 0) {
+            const uint32_t rr = r + lane;
+            if (rr < R) {
+                blk_nb = nb[rr];
+                blk_po = poff[rr];
+                blk_np = poff[rr + 1] - blk_po;
+                blk_p0 = blk_np > 0 ? pred[blk_po] : 0u;
+                blk_p1 = blk_np > 1 ? pred[blk_po + 1] : 0u;
+                blk_sp = spf[rr];
+            }
+        }
+        const int li = (int)(r & 63u);
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)blk_nb, li) & 3u;
+        const uint32_t po = (uint32_t)__builtin_amdgcn_readlane((int)blk_po, li);
+        const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)blk_np, li);
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)blk_p0, li);
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)blk_p1, li);
+        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)blk_sp, li);
+        if (np > 255u) {
+            z.status = kErrInDegree;
+            return;
+        }
+        // band placement (SPEC.md §3.1)
+        int32_t off = 0;
+        if (np) {
+            int32_t bm = INT32_MIN, barg = 0;
+            for (uint32_t s = 0; s < np; ++s) {
+                const uint32_t p = s == 0 ? p0 : s == 1 ? p1 : uni(pred[po + s]);
+                const PredRow pm = pred_meta(z, r, p);
+                if (pm.rmax > bm) bm = pm.rmax, barg = pm.rarg;
+            }
+            off = barg + 1 - kW / 2;
+            off = off < 0 ? 0 : off;
+            off = off > lim ? lim : off;
+        }
+        // predecessor terms (SPEC.md §3.2)
+        int32_t Mh0 = kNeg, Mh1 = kNeg, Dv0 = kNeg, Dv1 = kNeg;
+        uint32_t ms0 = 0, ms1 = 0, ds0 = 0, ds1 = 0, dx0 = 0, dx1 = 0;
+        for (uint32_t s = 0; s < np; ++s) {
+            const uint32_t p = s == 0 ? p0 : s == 1 ? p1 : uni(pred[po + s]);
+            const PredRow pm = pred_meta(z, r, p);
+            const int sh = off - pm.off;
+            int hA, hB, hC, dB, dC;
+            if (r - p <= (uint32_t)kRing) {
+                const int32_t *row = z.lds + (p % kRing) * 256;
+                hA = cell_lds<0>(row, sh - 1, lane);
+                hB = cell_lds<0>(row, sh, lane);
+                hC = cell_lds<0>(row, sh + 1, lane);
+                dB = cell_lds<2>(row, sh, lane);
+                dC = cell_lds<2>(row, sh + 1, lane);
+            } else {
+                const int32_t *row = spill + (size_t)g_sslot[p] * 256;
+                hA = cell_glb<0>(row, sh - 1, lane);
+                hB = cell_glb<0>(row, sh, lane);
+                hC = cell_glb<0>(row, sh + 1, lane);
+                dB = cell_glb<2>(row, sh, lane);
+                dC = cell_glb<2>(row, sh + 1, lane);
+            }
+            if (hA > Mh0) Mh0 = hA, ms0 = s;
+            if (hB > Mh1) Mh1 = hB, ms1 = s;
+            {
+                const int a = hB + kO + kE, b = dB + kE;
+                const int c = b > a ? b : a;
+                if (c > Dv0) Dv0 = c, ds0 = s, dx0 = b > a;
+            }
+            {
+                const int a = hC + kO + kE, b = dC + kE;
+                const int c = b > a ? b : a;
+                if (c > Dv1) Dv1 = c, ds1 = s, dx1 = b > a;
+            }
+        }
+        const int32_t j0 = off + t0, j1 = off + t1;
+        const bool v0 = j0 < (int32_t)m, v1 = j1 < (int32_t)m;
+        const uint32_t q0 = v0 ? rcode(z, (uint32_t)j0) : 0u;
+        const uint32_t q1 = v1 ? rcode(z, (uint32_t)j1) : 0u;
+        const int32_t src0 = j0 == 0 ? 0 : kO + kE * j0;
+        const int32_t src1 = kO + kE * j1;
+        uint32_t hc0, hc1;
+        int32_t mb0, mb1;
+        if (Mh0 >= src0) mb0 = Mh0, hc0 = HC_MPRED;
+        else mb0 = src0, hc0 = HC_MSRC, ms0 = 0;
+        if (Mh1 >= src1) mb1 = Mh1, hc1 = HC_MPRED;
+        else mb1 = src1, hc1 = HC_MSRC, ms1 = 0;
+        int32_t hp0 = mb0 + (base == q0 ? kMs : kXs);
+        int32_t hp1 = mb1 + (base == q1 ? kMs : kXs);
+        if (Dv0 > hp0) hp0 = Dv0, hc0 = HC_DEL;
+        if (Dv1 > hp1) hp1 = Dv1, hc1 = HC_DEL;
+        // in-row insertions (SPEC.md §3.4): exclusive prefix max of X = H' - E*t
+        const int32_t X0 = hp0 - kE * t0, X1 = hp1 - kE * t1;
+        const int32_t incl = wave_incl_max(max(X0, X1));
+        const int32_t Pex = wave_shr1(kNeg, incl);
+        const int32_t ex1 = max(Pex, X0);
+        const int32_t I0 = t0 == 0 ? kNeg : kO + kE * t0 + Pex;
+        const int32_t I1 = kO + kE * t1 + ex1;
+        const uint32_t iext1 = Pex > X0;
+        const uint32_t iext0 = (uint32_t)wave_shr1(0, (int)(ex1 > X1));
+        int32_t H0 = hp0, H1 = hp1;
+        if (I0 > H0) H0 = I0, hc0 = HC_INS;
+        if (I1 > H1) H1 = I1, hc1 = HC_INS;
+        uint32_t c0 = hc0 | (dx0 << 2) | (iext0 << 3);
+        uint32_t c1 = hc1 | (dx1 << 2) | (iext1 << 3);
+        if (!v0) H0 = kNeg, Dv0 = kNeg, c0 = 0, ms0 = 0, ds0 = 0;
+        if (!v1) H1 = kNeg, Dv1 = kNeg, c1 = 0, ms1 = 0, ds1 = 0;
+        // row max / argmax for the successors' band placement
+        const int32_t rm = wave_max(max(H0, H1));
+        const uint64_t hit = ballot(H0 == rm || H1 == rm);
+        const int L = (int)__builtin_ctzll(hit);
+        const int32_t hL = __builtin_amdgcn_readlane(H0, L);
+        const int32_t rarg = off + 2 * L + (hL == rm ? 0 : 1);
+        // free-end candidates (SPEC.md §3.5)
+        if (v0) {
+            const int32_t e = H0 + (j0 == (int32_t)m - 1 ? 0 : kO + kE * ((int32_t)m - 1 - j0));
+            if (e > bE) bE = e, bR = r, bJ = (uint32_t)j0;
+        }
+        if (v1) {
+            const int32_t e = H1 + (j1 == (int32_t)m - 1 ? 0 : kO + kE * ((int32_t)m - 1 - j1));
+            if (e > bE) bE = e, bR = r, bJ = (uint32_t)j1;
+        }
+        // traceback codes: 64 B per row (+256 B of predecessor slots if np > 1)
+        const uint32_t tof = r * 64u + nmulti * 256u;
+        trace[tof + lane] = (uint8_t)(c0 | (c1 << 4));
+        if (np > 1) {
+            if (nmulti >= z.d.mcap) {
+                z.status = kErrMulti;
+                return;
+            }
+            reinterpret_cast<uint32_t *>(trace + tof + 64)[lane] = ms0 | (ms1 << 8) | (ds0 << 16) | (ds1 << 24);
+            ++nmulti;
+        }
+        // the row itself: LDS ring (+ HBM spill) and its meta
+        int32_t *row = z.lds + (r % kRing) * 256;
+        row[lane] = H0;
+        row[64 + lane] = H1;
+        row[128 + lane] = Dv0;
+        row[192 + lane] = Dv1;
+        if (lane == 0) {
+            int32_t *mt = z.meta + (r % kRing) * 4;
+            mt[0] = off, mt[1] = rm, mt[2] = rarg;
+            g_roff[r] = off;
+            g_rmx[r] = rm;
+            g_rag[r] = rarg;
+            g_tof[r] = tof;
+        }
+        if (sp) {
+            if (nspill >= z.d.scap) {
+                z.status = kErrSpill;
+                return;
+            }
+            int32_t *srow = spill + (size_t)nspill * 256;
+            srow[lane] = H0;
+            srow[64 + lane] = H1;
+            srow[128 + lane] = Dv0;
+            srow[192 + lane] = Dv1;
+            if (lane == 0) g_sslot[r] = nspill;
+            ++nspill;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): ring row visible to the next row
+        __builtin_amdgcn_wave_barrier();
+    }
+    // lexicographic (max score, min row, min j) over the lanes' candidates
+    const int32_t best = wave_max(bE);
+    const uint32_t rsel = bE == best ? bR : 0x7FFFFFFFu;
+    const int32_t rmin = wave_min((int32_t)rsel);
+    const uint32_t jsel = (bE == best && bR == (uint32_t)rmin) ? bJ : 0x7FFFFFFFu;
+    const int32_t jmin = wave_min((int32_t)jsel);
+    er_out = (uint32_t)rmin;
+    ej_out = (uint32_t)jmin;
+    z.cells += (unsigned long long)R * (m < (uint32_t)kW ? m : (uint32_t)kW);
+    __syncthreads();
+}
+
+// ----------------------------------------------------------------------------
+// SPEC.md §4: traceback into one event per read base (lane 0 walks)
+// ----------------------------------------------------------------------------
+__device__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
+{
+    const uint32_t lane = threadIdx.x;
+    uint32_t *ev = P<uint32_t>(z, z.L.ev);
+    for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
+    const uint32_t *poff = P<uint32_t>(z, z.L.poff[z.cur]);
+    const uint32_t *pred = P<uint32_t>(z, z.L.pred[z.cur]);
+    const int32_t *g_roff = P<int32_t>(z, z.L.roff);
+    const uint32_t *g_tof = P<uint32_t>(z, z.L.tof);
+    const uint8_t *trace = P<uint8_t>(z, z.L.trace);
+    uint32_t lead_row = 0, lead_j = 0;
+    int32_t err = 0;
+    if (lane == 0) {
+        uint32_t r = er;
+        int32_t j = (int32_t)ej;
+        int st = 0;
+        uint64_t guard = 0;
+        const uint64_t lim = (uint64_t)z.R * 2 + (uint64_t)m * 2 + 16;
+        for (;;) {
+            if (++guard > lim) {
+                err = kErrTrace;
+                break;
+            }
+            const uint32_t t = (uint32_t)(j - g_roff[r]);
+            const uint32_t tof = g_tof[r];
+            const uint32_t c = (trace[tof + (t >> 1)] >> ((t & 1u) * 4u)) & 15u;
+            if (st == 0) {
+                const uint32_t hc = c & 3u;
+                if (hc == HC_MPRED) {
+                    ev[j] = (EV_ALN << 30) | r;
+                    const uint32_t np = poff[r + 1] - poff[r];
+                    const uint32_t s = np > 1 ? trace[tof + 64 + (t >> 1) * 4 + (t & 1u)] : 0u;
+                    r = pred[poff[r] + s];
+                    --j;
+                } else if (hc == HC_MSRC) {
+                    ev[j] = (EV_ALN << 30) | r;
+                    lead_row = r;
+                    lead_j = (uint32_t)j;
+                    break;
+                } else if (hc == HC_DEL) {
+                    st = 1;
+                } else {
+                    st = 2;
+                }
+            } else if (st == 1) {
+                const uint32_t np = poff[r + 1] - poff[r];
+                const uint32_t s = np > 1 ? trace[tof + 64 + (t >> 1) * 4 + 2 + (t & 1u)] : 0u;
+                st = (c >> 2) & 1u ? 1 : 0;
+                r = pred[poff[r] + s];
+            } else {
+                ev[j] = (EV_INS << 30) | r;
+                st = (c >> 3) & 1u ? 2 : 0;
+                --j;
+            }
+        }
+    }
+    err = __builtin_amdgcn_readfirstlane(err);
+    if (err) {
+        z.status = err;
+        return;
+    }
+    lead_row = uni(lead_row);
+    lead_j = uni(lead_j);
+    __syncthreads();
+    for (uint32_t j = lane; j < lead_j; j += 64) ev[j] = (EV_LEAD << 30) | lead_row;
+    __syncthreads();
+}
+
+// ----------------------------------------------------------------------------
+// SPEC.md §5: merge read k into the graph (double-buffered rebuild)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t col_start(const uint8_t *nb, uint32_t v)
+{
+    while (!(nb[v] & 4)) --v;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint32_t R)
+{
+    ++v;
+    while (v < R && !(nb[v] & 4)) ++v;
+    return v;
+}
+
+__device__ void merge(Z &z, uint32_t k, uint32_t m)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t R = z.R, nw = z.d.nw;
+    const int a = z.cur, b = a ^ 1;
+    const uint8_t *nb = P<uint8_t>(z, z.L.nb[a]);
+    const uint64_t *mem = P<uint64_t>(z, z.L.mem[a]);
+    const uint32_t *poff = P<uint32_t>(z, z.L.poff[a]);
+    const uint32_t *pred = P<uint32_t>(z, z.L.pred[a]);
+    uint8_t *nb2 = P<uint8_t>(z, z.L.nb[b]);
+    uint64_t *mem2 = P<uint64_t>(z, z.L.mem[b]);
+    uint32_t *poff2 = P<uint32_t>(z, z.L.poff[b]);
+    uint32_t *pred2 = P<uint32_t>(z, z.L.pred[b]);
+    const uint32_t *ev = P<uint32_t>(z, z.L.ev);
+    uint32_t *tgt = P<uint32_t>(z, z.L.tgt);
+    uint32_t *ipt = P<uint32_t>(z, z.L.ipt);
+    uint8_t *iinf = P<uint8_t>(z, z.L.iinf);
+    uint32_t *ifix = P<uint32_t>(z, z.L.ifix);
+    uint32_t *cnt = P<uint32_t>(z, z.L.cnt);
+    uint8_t *fixf = P<uint8_t>(z, z.L.fixf);
+    uint32_t *addp = P<uint32_t>(z, z.L.addp);
+    uint32_t *cntn = P<uint32_t>(z, z.L.cntn);
+
+    // M1: classify every read base, number the new nodes in read order
+    uint32_t K = 0;
+    for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        bool isnew = false;
+        uint32_t pt = 0, cs = 1, fix = kNone, t = 0, bq = 0;
+        if (j < m) {
+            bq = rcode(z, j);
+            if (R == 0) {
+                isnew = true;
+            } else {
+                const uint32_t e = ev[j], v = e & 0x3FFFFFFFu, kind = e >> 30;
+                if (kind == EV_ALN) {
+                    if ((nb[v] & 3u) == bq) {
+                        t = v;
+                    } else {
+                        const uint32_t s0 = col_start(nb, v), s1 = col_end(nb, v, R);
+                        uint32_t u = s0;
+                        while (u < s1 && (nb[u] & 3u) < bq) ++u;
+                        if (u < s1 && (nb[u] & 3u) == bq) {
+                            t = u;
+                        } else {
+                            isnew = true;
+                            pt = u;
+                            cs = u == s0;
+                            if (cs) fix = s0;
+                        }
+                    }
+                } else if (kind == EV_INS) {
+                    isnew = true;
+                    pt = col_end(nb, v, R);
+                } else {
+                    isnew = true;
+                    pt = col_start(nb, v);
+                }
+            }
+        }
+        const uint64_t bal = ballot(isnew);
+        const uint32_t idx = K + lanes_below(bal);
+        if (j < m) {
+            if (isnew) {
+                ipt[idx] = pt;
+                iinf[idx] = (uint8_t)(bq | (cs << 2));
+                ifix[idx] = fix;
+                tgt[j] = kNewBit | idx;
+            } else {
+                tgt[j] = t;
+            }
+        }
+        K += (uint32_t)__builtin_popcountll(bal);
+    }
+    const uint32_t R2 = R + K;
+    if (R2 > z.d.rcap) {
+        z.status = kErrRows;
+        return;
+    }
+    // M2: shift[x] = #new items with point <= x
+    for (uint32_t x = lane; x <= R; x += 64) cnt[x] = 0, fixf[x] = 0;
+    __syncthreads();
+    for (uint32_t i = lane; i < K; i += 64) {
+        atomicAdd(&cnt[ipt[i]], 1u);
+        if (ifix[i] != kNone) fixf[ifix[i]] = 1;
+    }
+    __syncthreads();
+    {
+        uint32_t carry = 0;
+        for (uint32_t x0 = 0; x0 <= R; x0 += 64) {
+            const uint32_t x = x0 + lane;
+            const uint32_t v = x <= R ? cnt[x] : 0u;
+            const uint32_t inc = (uint32_t)wave_incl_sum((int)v);
+            if (x <= R) cnt[x] = carry + inc;
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+    }
+    __syncthreads();
+    const uint32_t *shift = cnt;
+    auto newidx = [&](uint32_t t) -> uint32_t {
+        return (t & kNewBit) ? ipt[t & ~kNewBit] + (t & ~kNewBit) : t + shift[t];
+    };
+    // M3: at most one new in-edge per target of this read (dedup vs existing)
+    for (uint32_t x = lane; x < R2; x += 64) addp[x] = kNone;
+    __syncthreads();
+    for (uint32_t j = 1 + lane; j < m; j += 64) {
+        const uint32_t s = tgt[j - 1], d = tgt[j];
+        bool dup = false;
+        if (!(d & kNewBit) && !(s & kNewBit)) {
+            const uint32_t e1 = poff[d + 1];
+            for (uint32_t e = poff[d]; e < e1; ++e)
+                if (pred[e] == s) {
+                    dup = true;
+                    break;
+                }
+        }
+        if (!dup) addp[newidx(d)] = newidx(s);
+    }
+    __syncthreads();
+    // M4: rows of the new graph
+    for (uint32_t x = lane; x < R; x += 64) {
+        const uint32_t n = x + shift[x];
+        nb2[n] = fixf[x] ? (uint8_t)(nb[x] & 3u) : nb[x];
+        for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = mem[(size_t)x * nw + w];
+        cntn[n] = poff[x + 1] - poff[x] + (addp[n] != kNone ? 1u : 0u);
+    }
+    for (uint32_t i = lane; i < K; i += 64) {
+        const uint32_t n = ipt[i] + i;
+        nb2[n] = iinf[i];
+        for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = 0;
+        cntn[n] = addp[n] != kNone ? 1u : 0u;
+    }
+    __syncthreads();
+    for (uint32_t j = lane; j < m; j += 64) {
+        const uint32_t n = newidx(tgt[j]);
+        mem2[(size_t)n * nw + (k >> 6)] |= 1ull << (k & 63u);
+    }
+    {
+        uint32_t carry = 0;
+        for (uint32_t x0 = 0; x0 < R2; x0 += 64) {
+            const uint32_t x = x0 + lane;
+            const uint32_t v = x < R2 ? cntn[x] : 0u;
+            const uint32_t inc = (uint32_t)wave_incl_sum((int)v);
+            if (x < R2) poff2[x] = carry + inc - v;
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+        if (lane == 0) poff2[R2] = carry;
+        const uint32_t E2 = uni(carry);
+        if (E2 > z.d.ecap) {
+            z.status = kErrEdges;
+            return;
+        }
+        z.E = E2;
+    }
+    __syncthreads();
+    for (uint32_t x = lane; x < R; x += 64) {
+        const uint32_t n = x + shift[x];
+        uint32_t o = poff2[n];
+        const uint32_t e1 = poff[x + 1];
+        for (uint32_t e = poff[x]; e < e1; ++e) {
+            const uint32_t p = pred[e];
+            pred2[o++] = p + shift[p];
+        }
+        if (addp[n] != kNone) pred2[o] = addp[n];
+    }
+    for (uint32_t i = lane; i < K; i += 64) {
+        const uint32_t n = ipt[i] + i;
+        if (addp[n] != kNone) pred2[poff2[n]] = addp[n];
+    }
+    // M5: first/last rows of the reads
+    uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
+    for (uint32_t kk = lane; kk < k; kk += 64)
+        if (rfirst[kk] != kNone) {
+            rfirst[kk] += shift[rfirst[kk]];
+            rlast[kk] += shift[rlast[kk]];
+        }
+    if (lane == 0) {
+        rfirst[k] = newidx(tgt[0]);
+        rlast[k] = newidx(tgt[m - 1]);
+    }
+    z.R = R2;
+    z.cur = b;
+    __syncthreads();
+}
+
+// ----------------------------------------------------------------------------
+// SPEC.md §6: columns, per-column consensus and the consensus-match masks
+// ----------------------------------------------------------------------------
+__device__ uint32_t call_columns(Z &z, uint32_t n)
+{
+    const uint32_t lane = threadIdx.x;
+    const uint32_t R = z.R, nw = z.d.nw;
+    const uint8_t *nb = P<uint8_t>(z, z.L.nb[z.cur]);
+    const uint64_t *mem = P<uint64_t>(z, z.L.mem[z.cur]);
+    uint32_t *colof = P<uint32_t>(z, z.L.colof);
+    uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
+    uint8_t *cons = P<uint8_t>(z, z.L.cons);
+    uint64_t *cmask = P<uint64_t>(z, z.L.cmask);
+    const uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
+    uint32_t *rfc = P<uint32_t>(z, z.L.rfc), *rlc = P<uint32_t>(z, z.L.rlc);
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < R; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        const bool f = r < R && (nb[r] & 4);
+        const uint64_t bal = ballot(f);
+        const uint32_t c = carry + lanes_below(bal) + (f ? 1u : 0u) - 1u;
+        if (r < R) colof[r] = c;
+        if (f) colrow[c] = r;
+        carry += (uint32_t)__builtin_popcountll(bal);
+    }
+    const uint32_t ncols = carry;
+    if (lane == 0) colrow[ncols] = R;
+    __syncthreads();
+    for (uint32_t k = lane; k < n; k += 64) {
+        rfc[k] = rfirst[k] != kNone ? colof[rfirst[k]] : kNone;
+        rlc[k] = rfirst[k] != kNone ? colof[rlast[k]] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t c = lane; c < ncols; c += 64) {
+        const uint32_t a = colrow[c], e = colrow[c + 1];
+        uint32_t cnt[4] = {0, 0, 0, 0}, tot = 0, cov = 0;
+        for (uint32_t u = a; u < e; ++u) {
+            uint32_t pc = 0;
+            for (uint32_t w = 0; w < nw; ++w) pc += (uint32_t)__builtin_popcountll(mem[(size_t)u * nw + w]);
+            cnt[nb[u] & 3u] += pc;
+            tot += pc;
+        }
+        for (uint32_t k = 0; k < n; ++k) cov += (rfc[k] <= c && c <= rlc[k]) ? 1u : 0u;
+        uint32_t best = 0;
+        for (uint32_t bb = 1; bb < 4; ++bb)
+            if (cnt[bb] > cnt[best]) best = bb;
+        const uint32_t gap = cov - tot;
+        const uint32_t cb = cnt[best] >= gap ? best : 4u;
+        cons[c] = (uint8_t)cb;
+        uint32_t crow = kNone;
+        for (uint32_t u = a; u < e; ++u)
+            if ((nb[u] & 3u) == cb) crow = u;
+        for (uint32_t w = 0; w < nw; ++w) cmask[(size_t)c * nw + w] = crow != kNone ? mem[(size_t)crow * nw + w] : 0ull;
+    }
+    __syncthreads();
+    return ncols;
+}
+
+// ----------------------------------------------------------------------------
+// end_bspoa over the reads staged in rdoff/rdlen (main.c:492,571)
+// ----------------------------------------------------------------------------
+__device__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zseq)
+{
+    const uint32_t *rdoff = P<uint32_t>(z, z.L.rdoff), *rdlen = P<uint32_t>(z, z.L.rdlen);
+    uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
+    z.R = 0;
+    z.E = 0;
+    z.cur = 0;
+    if (threadIdx.x == 0) P<uint32_t>(z, z.L.poff[0])[0] = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t m = uni(rdlen[k]);
+        if (threadIdx.x == 0) rfirst[k] = rlast[k] = kNone;
+        __syncthreads();
+        if (m == 0) continue;
+        if (m > z.rdcap || m > z.d.lcap) {
+            z.status = kErrReadLen;
+            return 0;
+        }
+        load_read(z, zseq + uni(rdoff[k]), m);
+        if (z.R) {
+            uint32_t er, ej;
+            mark_spills(z);
+            dp_align(z, m, er, ej);
+            if (z.status) return 0;
+            traceback(z, m, er, ej);
+            if (z.status) return 0;
+        }
+        merge(z, k, m);
+        if (z.status) return 0;
+    }
+    return call_columns(z, n);
+}
+
+// main.c:580-612: largest i >= 1 whose 10-column window is a clean breakpoint
+__device__ bool bp_ok(const Z &z, uint32_t i, uint32_t nseq, uint32_t colrate)
+{
+    const uint32_t window = 10, minwin = 5, rowrate = 80, nw = z.d.nw;
+    const uint8_t *cons = P<uint8_t>(z, z.L.cons);
+    const uint64_t *cmask = P<uint64_t>(z, z.L.cmask);
+    uint32_t nogwin = 0, j;
+    for (j = i; j < i + window; ++j) {
+        if (cons[j] >= 4) {
+            if (nogwin) continue;
+            else break;
+        }
+        ++nogwin;
+        uint32_t colcnt = 0;
+        for (uint32_t w = 0; w < nw; ++w) colcnt += (uint32_t)__builtin_popcountll(cmask[(size_t)j * nw + w]);
+        if (colcnt * 100 < colrate * nseq) break;
+    }
+    if (j < i + window || nogwin < minwin) return false;
+    for (uint32_t k = 0; k < nseq; ++k) {
+        uint32_t rc = 0;
+        for (uint32_t jj = i; jj < i + window; ++jj)
+            if (cons[jj] < 4) rc += (uint32_t)(cmask[(size_t)jj * nw + (k >> 6)] >> (k & 63u)) & 1u;
+        if (rc * 100 < rowrate * nogwin) return false;
+    }
+    return true;
+}
+
+__device__ uint32_t find_breakpoint(const Z &z, uint32_t ncols, uint32_t nseq, uint32_t colrate)
+{
+    const uint32_t window = 10;
+    if (ncols <= window) return 0;  // SPEC.md §7 (main.c:580 would underflow)
+    for (int32_t top = (int32_t)(ncols - window); top >= 1; top -= 64) {
+        const int32_t cand = top - (int32_t)threadIdx.x;
+        const bool ok = cand >= 1 && bp_ok(z, (uint32_t)cand, nseq, colrate);
+        const uint64_t bal = ballot(ok);
+        if (bal) return (uint32_t)(top - (int32_t)__builtin_ctzll(bal));
+    }
+    return 0;
+}
+
+// emit the consensus of columns [0, i) (main.c:622-638); advance pos if flag
+__device__ void emit(Z &z, uint32_t i, uint32_t ncols, uint32_t n, bool flag, uint8_t *out, uint32_t &ol)
+{
+    const uint32_t lane = threadIdx.x, nw = z.d.nw;
+    const uint8_t *cons = P<uint8_t>(z, z.L.cons);
+    if (flag) {
+        const uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
+        const uint64_t *mem = P<uint64_t>(z, z.L.mem[z.cur]);
+        const uint32_t rend = i < ncols ? colrow[i] : z.R;
+        for (uint32_t r0 = 0; r0 < rend; r0 += 64) {
+            const uint32_t r = r0 + lane;
+            for (uint32_t w = 0; w < nw; ++w) {
+                const uint64_t x = r < rend ? mem[(size_t)r * nw + w] : 0ull;
+                const uint32_t kn = n - w * 64 < 64 ? n - w * 64 : 64;
+                for (uint32_t kb = 0; kb < kn; ++kb) {
+                    const uint32_t c = (uint32_t)__builtin_popcountll(ballot((x >> kb) & 1ull));
+                    if (lane == 0) z.pos[w * 64 + kb] += c;
+                }
+            }
+        }
+    }
+    for (uint32_t c0 = 0; c0 < i; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        const uint32_t cb = c < i ? cons[c] : 4u;
+        const uint64_t bal = ballot(cb < 4);
+        if (cb < 4) {
+            const uint32_t o = ol + lanes_below(bal);
+            if (o < z.d.outcap) out[o] = (uint8_t)"ACGT"[cb];
+        }
+        ol += (uint32_t)__builtin_popcountll(bal);
+    }
+    if (ol > z.d.outcap) z.status = kErrOut;
+    __syncthreads();
+}
+
+// tidy_msa_bspoa (main.c:572): column-major MSA with mrow = n + 4
+__device__ void write_msa(Z &z, uint32_t ncols, uint32_t n, uint8_t *msa)
+{
+    const uint32_t lane = threadIdx.x, nw = z.d.nw, mrow = n + 4;
+    const uint8_t *nb = P<uint8_t>(z, z.L.nb[z.cur]);
+    const uint64_t *mem = P<uint64_t>(z, z.L.mem[z.cur]);
+    const uint32_t *colof = P<uint32_t>(z, z.L.colof);
+    const uint8_t *cons = P<uint8_t>(z, z.L.cons);
+    const uint64_t tot = (uint64_t)ncols * mrow;
+    for (uint64_t x = lane; x < tot; x += 64) msa[x] = 4;
+    __syncthreads();
+    for (uint32_t r = lane; r < z.R; r += 64) {
+        uint8_t *cp = msa + (size_t)colof[r] * mrow;
+        for (uint32_t k = 0; k < n; ++k)
+            if ((mem[(size_t)r * nw + (k >> 6)] >> (k & 63u)) & 1ull) cp[k + 1] = nb[r] & 3u;
+    }
+    for (uint32_t c = lane; c < ncols; c += 64) msa[(size_t)c * mrow + n + 1] = cons[c];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
+{
+    extern __shared__ int32_t smem[];
+    const uint32_t zi = blockIdx.x;
+    if (zi >= a.nzmw) return;
+    const uint32_t lane = threadIdx.x;
+    Z z;
+    z.d = a.desc[zi];
+    zlayout(z.L, z.d);
+    z.ws = a.ws + z.d.ws_off;
+    z.seq = a.seq + z.d.seq_off;
+    z.lds = smem;
+    z.meta = smem + kRing * 256;
+    z.rd = reinterpret_cast<uint32_t *>(smem + kRing * 260);
+    z.pos = z.rd + a.lds_read_words;
+    z.rdcap = a.lds_read_words * 16;
+    z.status = kOk;
+    z.cells = 0;
+    const uint32_t n = z.d.n;
+    const uint32_t *soff = a.soff + z.d.seg0, *slen = a.slen + z.d.seg0;
+    uint32_t *rdoff = P<uint32_t>(z, z.L.rdoff), *rdlen = P<uint32_t>(z, z.L.rdlen);
+    uint8_t *out = a.out + z.d.out_off;
+    uint32_t ol = 0;
+
+    if (a.mode != kShred) {
+        // ccs_for (main.c:486-502) / single bspoa call: push every segment whole
+        for (uint32_t k = lane; k < n; k += 64) rdoff[k] = soff[k], rdlen[k] = slen[k];
+        __syncthreads();
+        const uint32_t ncols = run_poa(z, n, z.seq);
+        if (!z.status) {
+            emit(z, ncols, ncols, n, false, out, ol);
+            if (a.mode == kSinglePoa && !z.status) {
+                if ((uint64_t)ncols * (n + 4) > z.d.msacap) z.status = kErrOut;
+                else write_msa(z, ncols, n, a.msa + z.d.msa_off);
+                if (lane == 0) a.ncols[zi] = ncols;
+            }
+        }
+    } else if (n > a.lds_nmax) {
+        z.status = kErrReadLen;
+    } else {
+        // ccs_for2 (main.c:541-641)
+        const uint32_t addlen = 2000, minlen = 1000, initlen = 2000;
+        const uint32_t colrate = n < 10 ? 60u : 80u;
+        for (uint32_t k = lane; k < n; k += 64) z.pos[k] = 0;
+        __syncthreads();
+        bool flag = true;
+        while (flag && !z.status) {
+            uint32_t i = 0, ncols = 0;
+            for (uint32_t ws = initlen;; ws += addlen) {
+                bool fin = n < 3;
+                for (uint32_t k = 0; k < n && !fin; ++k)
+                    if (z.pos[k] + ws + minlen >= slen[k]) fin = true;
+                if (fin) flag = false;
+                for (uint32_t k = lane; k < n; k += 64) {
+                    rdoff[k] = soff[k] + z.pos[k];
+                    rdlen[k] = fin ? slen[k] - z.pos[k] : ws;
+                }
+                __syncthreads();
+                ncols = run_poa(z, n, z.seq);
+                if (z.status) break;
+                if (!flag) {
+                    i = ncols;
+                    break;
+                }
+                i = find_breakpoint(z, ncols, n, colrate);
+                if (i >= 1) break;
+            }
+            if (z.status) break;
+            emit(z, i, ncols, n, flag, out, ol);
+        }
+    }
+    if (lane == 0) {
+        a.out_len[zi] = ol;
+        a.status[zi] = z.status;
+        a.cells[zi] = z.cells;
+    }
+}
+
+}  // namespace ccsx
+
+extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s)
+{
+    if (lds_bytes > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&ccsx::ccsx_zmw_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(64), lds_bytes, s, *a);
+    return hipGetLastError();
+}

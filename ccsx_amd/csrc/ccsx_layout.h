@@ -1,0 +1,140 @@
+// ccsx_layout.h -- per-ZMW HBM workspace layout, shared by the host launcher
+// (sizing, offsets) and the device code (addressing).  See DESIGN.md §3.
+//
+// One ZMW owns one contiguous workspace slab.  Every capacity is derived from
+// S = sum of the ZMW's segment lengths (an upper bound on the rows and edges of
+// any POA the ZMW can build, SPEC.md §5) and n = number of segments.
+#pragma once
+#include <stdint.h>
+
+#ifndef CCSX_HD
+#if defined(__HIPCC__)
+#define CCSX_HD __host__ __device__
+#else
+#define CCSX_HD
+#endif
+#endif
+
+namespace ccsx {
+
+constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
+constexpr int kRing = 16;      // DP rows kept in LDS per wave
+constexpr int kNeg = -(1 << 29);
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
+enum Status : int32_t {
+    kOk = 0,
+    kErrRows = 1,      // graph rows exceed rcap
+    kErrEdges = 2,     // edges exceed ecap
+    kErrMulti = 3,     // multi-predecessor rows exceed mcap
+    kErrSpill = 4,     // spilled DP rows exceed scap
+    kErrInDegree = 5,  // node in-degree > 255
+    kErrReadLen = 6,   // pushed read longer than the LDS read buffer
+    kErrOut = 7,       // CCS longer than the output slab
+    kErrTrace = 8,     // traceback did not terminate (internal error)
+};
+
+enum Mode : int32_t { kShred = 0, kPrimitive = 1, kSinglePoa = 2 };
+
+struct ZmwDesc {
+    uint64_t seq_off;   // byte offset of the ZMW's sequence bytes in the seq arena
+    uint64_t ws_off;    // byte offset of the workspace slab (256-B aligned)
+    uint64_t out_off;   // byte offset of the CCS / consensus output slab
+    uint64_t msa_off;   // byte offset of the MSA output slab (kSinglePoa only)
+    uint32_t seg0;      // index of the first segment in the segment arrays
+    uint32_t n;         // number of segments (pushed reads)
+    uint32_t rcap, ecap, lcap, mcap, scap, nw;
+    uint32_t outcap;    // output slab capacity (bytes)
+    uint32_t msacap;    // MSA slab capacity (bytes)
+};
+
+struct ZLayout {
+    uint64_t nb[2], mem[2], poff[2], pred[2];
+    uint64_t roff, rmx, rag, tof, spf, sslot, trace, spill;
+    uint64_t ev, tgt, ipt, iinf, ifix, cnt, fixf, addp, cntn;
+    uint64_t colof, cons, cmask, colrow, rdoff, rdlen, rfirst, rlast, rfc, rlc;
+    uint64_t total;
+};
+
+CCSX_HD inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
+{
+    uint64_t o = 0;
+    auto take = [&](uint64_t bytes) {
+        uint64_t r = o;
+        o = align256(o + bytes);
+        return r;
+    };
+    for (int b = 0; b < 2; ++b) {
+        L.nb[b] = take(d.rcap);
+        L.mem[b] = take(uint64_t(d.rcap) * d.nw * 8);
+        L.poff[b] = take(uint64_t(d.rcap + 1) * 4);
+        L.pred[b] = take(uint64_t(d.ecap) * 4);
+    }
+    L.roff = take(uint64_t(d.rcap) * 4);
+    L.rmx = take(uint64_t(d.rcap) * 4);
+    L.rag = take(uint64_t(d.rcap) * 4);
+    L.tof = take(uint64_t(d.rcap) * 4);
+    L.spf = take(d.rcap);
+    L.sslot = take(uint64_t(d.rcap) * 4);
+    L.trace = take(uint64_t(d.rcap) * 64 + uint64_t(d.mcap) * 256);
+    L.spill = take(uint64_t(d.scap) * kW * 8);
+    L.ev = take(uint64_t(d.lcap) * 4);
+    L.tgt = take(uint64_t(d.lcap) * 4);
+    L.ipt = take(uint64_t(d.lcap) * 4);
+    L.iinf = take(d.lcap);
+    L.ifix = take(uint64_t(d.lcap) * 4);
+    L.cnt = take(uint64_t(d.rcap + 1) * 4);
+    L.fixf = take(d.rcap + 1);
+    L.addp = take(uint64_t(d.rcap) * 4);
+    L.cntn = take(uint64_t(d.rcap + 1) * 4);
+    L.colof = take(uint64_t(d.rcap) * 4);
+    L.cons = take(d.rcap);
+    L.cmask = take(uint64_t(d.rcap) * d.nw * 8);
+    L.colrow = take(uint64_t(d.rcap + 1) * 4);
+    L.rdoff = take(uint64_t(d.n) * 4);
+    L.rdlen = take(uint64_t(d.n) * 4);
+    L.rfirst = take(uint64_t(d.n) * 4);
+    L.rlast = take(uint64_t(d.n) * 4);
+    L.rfc = take(uint64_t(d.n) * 4);
+    L.rlc = take(uint64_t(d.n) * 4);
+    L.total = o;
+}
+
+// Capacities for a ZMW with segment lengths summing to S, longest segment
+// lmax, n segments.  Rows and edges are exact upper bounds (SPEC.md §5: each
+// read base creates at most one node and one in-edge); mcap/scap are sized
+// generously and checked at run time (kErrMulti / kErrSpill).
+CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n)
+{
+    d.n = n;
+    d.rcap = uint32_t(S + 16);
+    d.ecap = uint32_t(S + n + 16);
+    d.lcap = lmax + 16;
+    d.mcap = d.rcap / 2 + 64;
+    d.scap = d.rcap / 4 + 64;
+    d.nw = (n + 63) / 64 ? (n + 63) / 64 : 1;
+    d.outcap = uint32_t(S + 16);
+}
+
+struct KArgs {
+    const uint8_t *seq;
+    const uint32_t *soff;  // segment offset relative to the ZMW's seq_off
+    const uint32_t *slen;
+    const ZmwDesc *desc;
+    uint8_t *ws;
+    uint8_t *out;
+    uint8_t *msa;
+    uint32_t *out_len;
+    uint32_t *ncols;
+    int32_t *status;
+    unsigned long long *cells;
+    int32_t mode;
+    uint32_t nzmw;
+    uint32_t lds_read_words;
+    uint32_t lds_nmax;
+};
+
+}  // namespace ccsx

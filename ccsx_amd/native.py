@@ -1,0 +1,253 @@
+"""ctypes bindings of libccsx_amd.so (include/ccsx_gpu.h, ccsx_host.h, ccsx_seqio.h).
+
+The GPU engine has no CPU fallback: if the library is missing, or no GPU is
+present, every call that needs it raises.  Host-side helpers (ccs_prepare,
+reverse complement, the synthetic ZMW source, the subread reader) run on the
+CPU and work without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libccsx_amd.so")
+
+MODE_SHRED = 0
+MODE_PRIMITIVE = 1
+
+# every symbol the public headers declare (checked by tests/test_abi.py)
+EXPORTS = {
+    "ccsx_gpu.h": ["ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
+                   "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes"],
+    "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
+    "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw"],
+    "ccsx_seqio.h": ["ccsx_reader_open", "ccsx_reader_next", "ccsx_reader_close"],
+}
+
+
+class ZmwIn(C.Structure):
+    _fields_ = [("seqs", C.c_char_p), ("seg_off", C.POINTER(C.c_uint32)), ("seg_len", C.POINTER(C.c_uint32)),
+                ("nseg", C.c_uint32)]
+
+
+class ZmwOut(C.Structure):
+    _fields_ = [("ccs", C.c_void_p), ("len", C.c_uint32), ("status", C.c_int32), ("cells", C.c_uint64)]
+
+
+class PairAln(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("qb", "qe", "tb", "te", "mat", "mis", "ins", "del_", "aln", "score")]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        L.ccsx_gpu_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.ccsx_gpu_close.argtypes = [C.c_void_p]
+        L.ccsx_gpu_error.argtypes = [C.c_void_p]
+        L.ccsx_gpu_error.restype = C.c_char_p
+        L.ccsx_gpu_status_str.argtypes = [C.c_int32]
+        L.ccsx_gpu_status_str.restype = C.c_char_p
+        L.ccsx_gpu_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwIn), C.c_size_t, C.POINTER(ZmwOut)]
+        L.ccsx_gpu_stage.argtypes = [C.c_void_p, C.POINTER(ZmwIn), C.c_size_t]
+        L.ccsx_gpu_launch.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_float)]
+        L.ccsx_gpu_fetch.argtypes = [C.c_void_p, C.POINTER(ZmwOut)]
+        L.ccsx_gpu_staged_bytes.argtypes = [C.c_void_p]
+        L.ccsx_gpu_staged_bytes.restype = C.c_uint64
+        L.ccsx_revcomp.argtypes = [C.c_char_p, C.c_uint32]
+        L.ccsx_prepare.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
+                                   C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]
+        L.ccsx_prepare.restype = C.c_uint32
+        L.ccsx_prepare_apply.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint32)]
+        L.ccsx_prepare_apply.restype = C.c_uint32
+        L.ccsx_pairwise.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32]
+        L.ccsx_pairwise.restype = PairAln
+        L.ccsx_synth_zmw.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_char_p,
+                                     C.POINTER(C.c_uint32), C.c_char_p]
+        L.ccsx_synth_zmw.restype = C.c_uint64
+        L.ccsx_reader_open.argtypes = [C.c_char_p, C.c_int]
+        L.ccsx_reader_open.restype = C.c_void_p
+        L.ccsx_reader_next.argtypes = [C.c_void_p] + [C.POINTER(C.c_char_p)] * 2 + [C.POINTER(C.c_void_p),
+                                                                                     C.POINTER(C.POINTER(C.c_uint32))]
+        L.ccsx_reader_close.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def _p32(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+# ---------------------------------------------------------------- host helpers
+def revcomp(seq: bytes) -> bytes:
+    b = C.create_string_buffer(bytes(seq), len(seq))
+    lib().ccsx_revcomp(b, len(seq))
+    return b.raw[:len(seq)]
+
+
+def synth_zmw(seed: int, hole: int, L: int, passes: int):
+    """Synthetic ZMW: returns (list of subread bytes, true insert bytes)."""
+    cap = passes * (2 * L + 16) + 16
+    out = C.create_string_buffer(cap)
+    lens = np.zeros(passes, dtype=np.uint32)
+    ins = C.create_string_buffer(L + 1)
+    lib().ccsx_synth_zmw(seed, hole, L, passes, out, _p32(lens), ins)
+    raw = out.raw
+    subs, o = [], 0
+    for n in lens:
+        subs.append(raw[o:o + int(n)])
+        o += int(n)
+    return subs, ins.raw[:L]
+
+
+@dataclass
+class Prepared:
+    """One ZMW after ccs_prepare + strand flip: segments are slices of seqs."""
+    seqs: bytes
+    offs: np.ndarray
+    lens: np.ndarray
+
+
+def prepare(subreads: list[bytes]) -> Prepared:
+    """ccs_prepare (main.c:344-453) + in-place reverse complement of reverse segments."""
+    seqs = b"".join(subreads)
+    buf = C.create_string_buffer(seqs, len(seqs) + 1)
+    lens = _u32([len(s) for s in subreads])
+    n = len(subreads)
+    so = np.zeros(max(n, 1), dtype=np.uint32)
+    sl = np.zeros(max(n, 1), dtype=np.uint32)
+    ns = lib().ccsx_prepare_apply(buf, _p32(lens), n, _p32(so), _p32(sl))
+    return Prepared(buf.raw[:len(seqs)], so[:ns].copy(), sl[:ns].copy())
+
+
+def prepare_segments(subreads: list[bytes]):
+    """ccs_prepare only: (offs, lens, reverse flags) into the concatenated subreads."""
+    seqs = b"".join(subreads)
+    lens = _u32([len(s) for s in subreads])
+    n = len(subreads)
+    so = np.zeros(max(n, 1), dtype=np.uint32)
+    sl = np.zeros(max(n, 1), dtype=np.uint32)
+    rv = np.zeros(max(n, 1), dtype=np.uint8)
+    ns = lib().ccsx_prepare(seqs, _p32(lens), n, _p32(so), _p32(sl), rv.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return so[:ns].copy(), sl[:ns].copy(), rv[:ns].copy()
+
+
+def pairwise(q: bytes, t: bytes) -> dict:
+    r = lib().ccsx_pairwise(q, len(q), t, len(t))
+    return {n if n != "del_" else "del": getattr(r, n) for n, _ in PairAln._fields_}
+
+
+def read_zmws(path: str, is_bam: bool = False):
+    """Yield (movie, hole, [subreads]) per kseq_zmw_read (seqio.h:152-201); stops at the first -1."""
+    L = lib()
+    r = L.ccsx_reader_open(path.encode(), 1 if is_bam else 0)
+    if not r:
+        raise OSError(f"cannot open {path}")
+    try:
+        mv, hl = C.c_char_p(), C.c_char_p()
+        sq = C.c_void_p()
+        ln = C.POINTER(C.c_uint32)()
+        while True:
+            n = L.ccsx_reader_next(r, C.byref(mv), C.byref(hl), C.byref(sq), C.byref(ln))
+            if n < 0:
+                break
+            lens = [ln[i] for i in range(n)]
+            raw = C.string_at(sq, sum(lens))
+            subs, o = [], 0
+            for x in lens:
+                subs.append(raw[o:o + x])
+                o += x
+            yield mv.value.decode(), hl.value.decode(), subs
+    finally:
+        L.ccsx_reader_close(r)
+
+
+# ---------------------------------------------------------------- GPU engine
+class GpuError(RuntimeError):
+    pass
+
+
+class Engine:
+    """A context on one HIP device: the batched C-ABI of include/ccsx_gpu.h."""
+
+    def __init__(self, device: int = 0):
+        self._L = lib()
+        self._ctx = C.c_void_p()
+        if self._L.ccsx_gpu_open(device, C.byref(self._ctx)) != 0:
+            raise GpuError(f"cannot open HIP device {device}")
+        self._keep = None
+        self._nz = 0
+
+    def close(self):
+        if self._ctx:
+            self._L.ccsx_gpu_close(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, what: str):
+        raise GpuError(f"{what}: {self._L.ccsx_gpu_error(self._ctx).decode()}")
+
+    @staticmethod
+    def _build_in(zmws: list[Prepared]):
+        arr = (ZmwIn * max(len(zmws), 1))()
+        keep = []
+        for i, z in enumerate(zmws):
+            offs, lens = _u32(z.offs), _u32(z.lens)
+            keep += [z.seqs, offs, lens]
+            arr[i].seqs = z.seqs
+            arr[i].seg_off = _p32(offs)
+            arr[i].seg_len = _p32(lens)
+            arr[i].nseg = len(lens)
+        return arr, keep
+
+    def stage(self, zmws: list[Prepared]) -> None:
+        arr, keep = self._build_in(zmws)
+        if self._L.ccsx_gpu_stage(self._ctx, arr, len(zmws)) != 0:
+            self._err("ccsx_gpu_stage")
+        self._keep = (arr, keep)
+        self._nz = len(zmws)
+
+    def launch(self, mode: int = MODE_SHRED) -> float:
+        ms = C.c_float(0)
+        if self._L.ccsx_gpu_launch(self._ctx, mode, C.byref(ms)) != 0:
+            self._err("ccsx_gpu_launch")
+        return ms.value
+
+    def fetch(self):
+        out = (ZmwOut * max(self._nz, 1))()
+        rc = self._L.ccsx_gpu_fetch(self._ctx, out)
+        if rc != 0:
+            self._err("ccsx_gpu_fetch")
+        res = []
+        for i in range(self._nz):
+            o = out[i]
+            res.append((C.string_at(o.ccs, o.len) if o.len else b"", o.status, o.cells))
+        return res
+
+    def run(self, zmws: list[Prepared], mode: int = MODE_SHRED):
+        """stage + launch + fetch: returns [(ccs bytes, status, cells)]."""
+        self.stage(zmws)
+        self.launch(mode)
+        return self.fetch()
+
+    def staged_bytes(self) -> int:
+        return int(self._L.ccsx_gpu_staged_bytes(self._ctx))

@@ -1,0 +1,74 @@
+/*
+ * ccsx_gpu.h -- batched C-ABI of the MI355X consensus engine.
+ *
+ * Replaces step 1 of ccsx's 3-stage pipeline (main.c:698-706):
+ *
+ *     kt_for(p->nthreads, split_subread ? ccs_for2 : ccs_for, in, n_zmws);
+ *
+ * with one call per chunk of ZMWs.  The caller runs ccs_prepare()
+ * (main.c:344-453) and the strand flip (main.c:471-476 / 527-531) on its CPU
+ * threads and passes, per ZMW, the strand-normalised segments in push order
+ * (template, template-1 .. 0, template+1 .. n-1).  Everything from there
+ * (shredding main.c:541-641 or the -P single POA main.c:486-502, i.e. every
+ * beg/push/end/tidy_msa_bspoa call, the breakpoint scan and the CCS emission)
+ * runs on the GPU.  Scoring is main.c:841-849's (M=2 X=-6 O=-3 E=-2,
+ * bandwidth 128); SPEC.md defines the POA.
+ *
+ * Ownership: input buffers belong to the caller and are only read during the
+ * call.  Output CCS strings live in a context-owned arena, valid until the
+ * next ccsx_gpu_run / ccsx_gpu_fetch on the same context.
+ * Errors: every function returns 0 on success, < 0 on error; the message is
+ * ccsx_gpu_error(ctx).  The reference has no recoverable errors, so callers
+ * treat any error as fatal.
+ * Threading: one context per device; a context is used by one host thread.
+ */
+#ifndef CCSX_GPU_H
+#define CCSX_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ccsx_ctx ccsx_ctx;
+
+enum { CCSX_MODE_SHRED = 0, CCSX_MODE_PRIMITIVE = 1 };
+
+typedef struct {
+    const char *seqs;         /* the ZMW's bases (ASCII), segments are slices of it */
+    const uint32_t *seg_off;  /* nseg offsets into seqs, in push order */
+    const uint32_t *seg_len;  /* nseg lengths */
+    uint32_t nseg;
+} ccsx_zmw_in;
+
+typedef struct {
+    const char *ccs;          /* ASCII CCS (not NUL-terminated), ctx-owned */
+    uint32_t len;             /* 0 = no CCS (main.c:713 writes nothing) */
+    int32_t status;           /* 0 ok; see ccsx_gpu_status_str */
+    uint64_t cells;           /* DP cells computed for this ZMW */
+} ccsx_zmw_out;
+
+/* Open a context on HIP device `device`. */
+int ccsx_gpu_open(int device, ccsx_ctx **ctx);
+void ccsx_gpu_close(ccsx_ctx *ctx);
+const char *ccsx_gpu_error(const ccsx_ctx *ctx);
+const char *ccsx_gpu_status_str(int32_t status);
+
+/* One chunk: stage + launch + fetch (replaces kt_for(ccs_for2/ccs_for)). */
+int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out);
+
+/* The same in three steps, so inputs can stay resident in HBM across launches
+ * (used by bench.py).  ccsx_gpu_launch returns the kernel time measured with
+ * HIP events on the context's stream. */
+int ccsx_gpu_stage(ccsx_ctx *ctx, const ccsx_zmw_in *z, size_t nz);
+int ccsx_gpu_launch(ccsx_ctx *ctx, int mode, float *kernel_ms);
+int ccsx_gpu_fetch(ccsx_ctx *ctx, ccsx_zmw_out *out);
+
+/* Device bytes the staged batch occupies (workspace + arenas). */
+uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

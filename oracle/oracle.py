@@ -1,0 +1,100 @@
+"""ctypes bindings of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, as the checker.  The product (ccsx_amd/) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            import sys
+            sys.path.insert(0, os.path.dirname(_HERE))
+            from ccsx_amd.build import build_oracle
+            build_oracle()
+        L = C.CDLL(LIB_PATH)
+        L.opoa_init.argtypes = [C.c_int] * 5
+        L.opoa_init.restype = C.c_void_p
+        L.opoa_free.argtypes = [C.c_void_p]
+        L.opoa_beg.argtypes = [C.c_void_p]
+        L.opoa_push.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32]
+        L.opoa_end.argtypes = [C.c_void_p]
+        L.opoa_tidy_msa.argtypes = [C.c_void_p]
+        L.opoa_cns.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+        L.opoa_cns.restype = C.c_uint32
+        L.opoa_msa.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]
+        L.opoa_msa.restype = C.c_uint32
+        L.opoa_cells.argtypes = [C.c_void_p]
+        L.opoa_cells.restype = C.c_uint64
+        L.opoa_nrows.argtypes = [C.c_void_p]
+        L.opoa_nrows.restype = C.c_uint32
+        L.ocsx_zmw.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                               C.c_uint32, C.c_char_p]
+        L.ocsx_zmw.restype = C.c_size_t
+        if hasattr(L, "ocsx_batch"):
+            L.ocsx_batch.argtypes = [C.c_int, C.c_int, C.c_uint32, C.POINTER(C.c_char_p),
+                                     C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.POINTER(C.c_uint32)),
+                                     C.POINTER(C.c_uint32), C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                                     C.POINTER(C.c_uint64)]
+        _lib = L
+    return _lib
+
+
+class Poa:
+    """The oracle's bspoa-like object (SPEC.md) with main.c's parameters."""
+
+    def __init__(self, M=2, X=-6, O=-3, E=-2, W=128):
+        self._L = lib()
+        self._g = self._L.opoa_init(M, X, O, E, W)
+
+    def __del__(self):
+        try:
+            self._L.opoa_free(self._g)
+        except Exception:
+            pass
+
+    def poa(self, reads: list[bytes]):
+        """beg + push* + end + tidy: returns (cns codes, msa [ncols, nseq+4] uint8)."""
+        L = self._L
+        L.opoa_beg(self._g)
+        for r in reads:
+            L.opoa_push(self._g, r, len(r))
+        L.opoa_end(self._g)
+        L.opoa_tidy_msa(self._g)
+        p = C.c_void_p()
+        n = L.opoa_cns(self._g, C.byref(p))
+        cns = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (n,)).copy() if n else np.zeros(0, np.uint8)
+        ip, cp, mrow = C.c_void_p(), C.c_void_p(), C.c_uint32()
+        nc = L.opoa_msa(self._g, C.byref(ip), C.byref(cp), C.byref(mrow))
+        if nc:
+            msa = np.ctypeslib.as_array(C.cast(cp, C.POINTER(C.c_uint8)), (nc * mrow.value,)).copy()
+            msa = msa.reshape(nc, mrow.value)
+        else:
+            msa = np.zeros((0, len(reads) + 4), np.uint8)
+        return cns, msa
+
+    def zmw(self, seqs: bytes, offs, lens, mode: int = 0) -> bytes:
+        """ccs_for2 (mode 0) / ccs_for (mode 1) on strand-normalised segments."""
+        offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = C.create_string_buffer(int(lens.sum()) + 16)
+        n = self._L.ocsx_zmw(self._g, mode, seqs, offs.ctypes.data_as(C.POINTER(C.c_uint32)),
+                             lens.ctypes.data_as(C.POINTER(C.c_uint32)), len(lens), out)
+        return out.raw[:n]
+
+    def cells(self) -> int:
+        return int(self._L.opoa_cells(self._g))
+
+    def nrows(self) -> int:
+        return int(self._L.opoa_nrows(self._g))
