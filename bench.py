@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""bench.py -- throughput of the ccsx consensus hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "B"): 1,000 synthetic ZMWs per GPU, 10 kb
+insert x 8 passes, 10 % PacBio-like error (6 % ins / 3 % del / 1 % sub),
+default shredded mode.  A "step" is one launch of the hot path over the whole
+batch, inputs (post-ccs_prepare, strand-normalised segments) already resident
+in HBM.  Each rank processes its own 1,000 holes (weak scaling, no collective
+on the data path); torch.distributed (gloo) is used only for the barrier and
+the max-over-ranks time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D]
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §6 for the roofline model and
+profiles/ for the rocprofv3 summaries these numbers are checked against.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# SURVEY.md §8d workloads (per GPU).  B is the metric's configuration.
+CONFIGS = {
+    "B": dict(workload="B: 1000 ZMWs x 10 kb insert x 8 passes, 10% error, shredded (default) mode",
+              nzmw=1000, L=10000, passes=8, mode=0),
+    "C": dict(workload="C: 1000 ZMWs x 20 kb insert x 5 passes, 10% error, primitive (-P) mode",
+              nzmw=1000, L=20000, passes=5, mode=1),
+    "D": dict(workload="D: 10000 ZMWs x 2 kb insert x 30 passes, 10% error, shredded mode",
+              nzmw=10000, L=2000, passes=30, mode=0),
+}
+SEED = 20201104
+# gfx950 integer VALU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 int32 lane-ops/s
+# (MI355X_MICROARCH.md: SIMD-32, wave64 in 2 cycles); 10 int ops per DP cell
+#  -> 7.86e12 cells/s.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+OPS_PER_CELL = 10
+
+
+def make_batch(cfg: dict, rank: int):
+    import ccsx_amd as cx
+    zs = []
+    base = rank * cfg["nzmw"]
+    for h in range(base, base + cfg["nzmw"]):
+        subs, _ = cx.synth_zmw(SEED, h, cfg["L"], cfg["passes"])
+        zs.append(cx.prepare(subs))
+    return zs
+
+
+def cpu_baseline(zs, cfg: dict, budget_s: float = 15.0):
+    """The oracle (C restatement, pthreads, kt_for-style) on a bounded sample."""
+    from oracle import oracle as orc
+    threads = max(1, min(len(os.sched_getaffinity(0)), 16))
+    # estimate per-ZMW CPU cost on a small probe, then size the sample
+    probe = zs[: max(1, threads)]
+    _, _, dt = orc.batch(probe, cfg["mode"], threads)
+    per_zmw_cpu = dt * threads / len(probe)
+    n = int(max(threads, min(len(zs), budget_s / max(per_zmw_cpu, 1e-6))))
+    n = max(threads, (n // threads) * threads)
+    sample = zs[:n]
+    _, cells, dt = orc.batch(sample, cfg["mode"], threads)
+    return {"value": round(n / dt, 3), "unit": "ZMWs/s", "cores": threads, "kind": "port",
+            "gcups": round(sum(cells) / dt / 1e9, 4),
+            "sample": f"{n} ZMWs of the same workload, oracle/poa_oracle.c (C restatement of SPEC.md + "
+                      f"main.c:510-647) on {threads} pthreads; bsalign/ccsx itself is unbuildable here"}
+
+
+def load_traffic(cfg_key: str):
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+        return t.get(cfg_key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    ap.add_argument("--nzmw", type=int, default=0, help="override ZMWs per GPU (testing only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.nzmw:
+        cfg["nzmw"] = args.nzmw
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    import ccsx_amd as cx
+    zs = make_batch(cfg, rank)
+    eng = cx.Engine(local)
+    eng.stage(zs)
+    for _ in range(args.warmup):
+        eng.launch(cfg["mode"])
+    res = eng.fetch()
+    cells_per_step = sum(r[2] for r in res)
+    bad = [i for i, r in enumerate(res) if r[1] != 0]
+    if bad:
+        raise SystemExit(f"device status != 0 for {len(bad)} ZMWs")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        kernel_ms.append(eng.launch(cfg["mode"]))  # synchronises on the stream's end event
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([float(cells_per_step)], dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        cells_total_step = float(c.item())
+    else:
+        cells_total_step = float(cells_per_step)
+
+    if rank == 0:
+        n_total = cfg["nzmw"] * world * args.steps
+        value = n_total / elapsed
+        avg_launch_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        # roofline for the dominant kernel (ccsx_zmw_kernel, the only kernel):
+        # algorithmic int ops per launch / average launch duration (HIP events)
+        achieved = cells_per_step * OPS_PER_CELL / avg_launch_s / 1e12
+        out = {
+            "metric": "CCS ZMWs/sec (whole node)",
+            "value": round(value, 3),
+            "unit": "ZMWs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (SURVEY.md §8d generator, seed 20201104, per-rank hole ranges)",
+            "config": {"workload": cfg["workload"], "zmws_per_gpu": cfg["nzmw"], "insert_len": cfg["L"],
+                       "passes": cfg["passes"], "mode": "shredded" if cfg["mode"] == 0 else "primitive",
+                       "parallelism": f"hole-batch sharding x{world}, no collectives"},
+            "gcups": round(cells_total_step * args.steps / elapsed / 1e9, 3),
+            "cells_per_step": int(cells_total_step),
+            "roofline": {"bound": "valu-int32", "achieved": round(achieved, 4), "peak": round(VALU_PEAK_TOPS, 2),
+                         "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 5),
+                         "traffic": load_traffic(args.config),
+                         "kernel": "ccsx_zmw_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                         "ops_per_cell": OPS_PER_CELL},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(zs, cfg)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

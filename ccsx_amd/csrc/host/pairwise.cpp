@@ -3,7 +3,7 @@
 // ccsx_pairwise stands in for bsalign's kmer_striped_seqedit_pairwise(13, ...)
 // (called at main.c:264), which is un-vendored.  SPEC.md §8 defines it: k=13
 // exact-seed diagonal vote, then a banded local alignment (match +1,
-// mismatch -1, gap -1) around the winning diagonal.  It only decides strand
+// mismatch -2, gap -2) around the winning diagonal.  It only decides strand
 // and trimming of abnormal-length subreads on the host; it is not on the GPU
 // hot path.
 #include <algorithm>
@@ -87,9 +87,9 @@ ccsx_pairaln ccsx_pairwise(const uint8_t *q, uint32_t qlen, const uint8_t *t, ui
             const int64_t j = (int64_t)i + d0 - kHalfBand + k;
             if (j < 0 || j >= (int64_t)tlen) continue;
             // diag: (i-1, j-1) same k; up: (i-1, j) -> k+1; left: (i, j-1) -> k-1
-            const int32_t diag = (i > 0 && j > 0 ? Hprev[k + 1] : 0) + (q[i] < 4 && q[i] == t[j] ? 1 : -1);
-            const int32_t up = (i > 0 && k + 1 < BW ? Hprev[k + 2] : 0) - 1;
-            const int32_t left = (k > 0 ? Hcur[k] : 0) - 1;
+            const int32_t diag = (i > 0 && j > 0 ? Hprev[k + 1] : 0) + (q[i] < 4 && q[i] == t[j] ? 1 : -2);
+            const int32_t up = (i > 0 && k + 1 < BW ? Hprev[k + 2] : 0) - 2;
+            const int32_t left = (k > 0 ? Hcur[k] : 0) - 2;
             int32_t v = 0;
             uint8_t dir = 0;
             if (diag > v) v = diag, dir = 1;

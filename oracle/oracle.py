@@ -42,7 +42,7 @@ def lib() -> C.CDLL:
         L.ocsx_zmw.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                C.c_uint32, C.c_char_p]
         L.ocsx_zmw.restype = C.c_size_t
-        if hasattr(L, "ocsx_batch"):
+        if True:
             L.ocsx_batch.argtypes = [C.c_int, C.c_int, C.c_uint32, C.POINTER(C.c_char_p),
                                      C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.POINTER(C.c_uint32)),
                                      C.POINTER(C.c_uint32), C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
@@ -98,3 +98,37 @@ class Poa:
 
     def nrows(self) -> int:
         return int(self._L.opoa_nrows(self._g))
+
+
+def batch(zmws, mode: int = 0, nthreads: int = 1):
+    """Run ocsx_zmw over prepared ZMWs on nthreads pthreads.
+
+    zmws: objects with .seqs (bytes), .offs, .lens.  Returns (list of CCS bytes,
+    list of cells, wall seconds)."""
+    import time
+    L = lib()
+    n = len(zmws)
+    keep = []
+    seqs = (C.c_char_p * n)()
+    offs = (C.POINTER(C.c_uint32) * n)()
+    lens = (C.POINTER(C.c_uint32) * n)()
+    nseg = (C.c_uint32 * n)()
+    outs = (C.c_char_p * n)()
+    bufs = []
+    for i, z in enumerate(zmws):
+        o = np.ascontiguousarray(z.offs, dtype=np.uint32)
+        ln = np.ascontiguousarray(z.lens, dtype=np.uint32)
+        keep += [o, ln, z.seqs]
+        seqs[i] = z.seqs
+        offs[i] = o.ctypes.data_as(C.POINTER(C.c_uint32))
+        lens[i] = ln.ctypes.data_as(C.POINTER(C.c_uint32))
+        nseg[i] = len(ln)
+        b = C.create_string_buffer(int(ln.sum()) + 16)
+        bufs.append(b)
+        outs[i] = C.cast(b, C.c_char_p)
+    olen = (C.c_size_t * n)()
+    cells = (C.c_uint64 * n)()
+    t = time.perf_counter()
+    L.ocsx_batch(mode, nthreads, n, seqs, offs, lens, nseg, outs, olen, cells)
+    dt = time.perf_counter() - t
+    return [bufs[i].raw[:olen[i]] for i in range(n)], [int(cells[i]) for i in range(n)], dt

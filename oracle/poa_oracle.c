@@ -647,3 +647,54 @@ size_t ocsx_zmw(opoa_t *g, int mode, const char *seqs, const uint32_t *offs,
     out[ol] = 0;
     return ol;
 }
+
+/* ------------------------------------------------------------------------
+ * ocsx_batch: kt_for-style CPU run of ocsx_zmw over many ZMWs with nthreads
+ * pthreads (kthread.c:24-65 semantics: dynamic work sharing, one POA object per
+ * thread).  This is what "ccsx -j N" spends its step-1 time on; bench.py's
+ * cpu_baseline leg times it.
+ * ------------------------------------------------------------------------ */
+#include <pthread.h>
+
+typedef struct {
+    int mode;
+    uint32_t nz;
+    const char **seqs;
+    const uint32_t **offs, **lens;
+    const uint32_t *nseg;
+    char **out;
+    size_t *olen;
+    uint64_t *cells;
+    uint32_t next;
+    pthread_mutex_t mu;
+} batch_t;
+
+static void *batch_worker(void *arg)
+{
+    batch_t *b = arg;
+    opoa_t *g = opoa_init(2, -6, -3, -2, 128);
+    for (;;) {
+        pthread_mutex_lock(&b->mu);
+        uint32_t i = b->next++;
+        pthread_mutex_unlock(&b->mu);
+        if (i >= b->nz) break;
+        uint64_t c0 = g->cells;
+        b->olen[i] = ocsx_zmw(g, b->mode, b->seqs[i], b->offs[i], b->lens[i], b->nseg[i], b->out[i]);
+        b->cells[i] = g->cells - c0;
+    }
+    opoa_free(g);
+    return NULL;
+}
+
+void ocsx_batch(int mode, int nthreads, uint32_t nz, const char **seqs, const uint32_t **offs,
+                const uint32_t **lens, const uint32_t *nseg, char **out, size_t *olen, uint64_t *cells)
+{
+    batch_t b = {mode, nz, seqs, offs, lens, nseg, out, olen, cells, 0};
+    pthread_mutex_init(&b.mu, NULL);
+    if (nthreads < 1) nthreads = 1;
+    pthread_t *tid = malloc(sizeof(pthread_t) * (size_t)nthreads);
+    for (int t = 0; t < nthreads; ++t) pthread_create(&tid[t], NULL, batch_worker, &b);
+    for (int t = 0; t < nthreads; ++t) pthread_join(tid[t], NULL);
+    free(tid);
+    pthread_mutex_destroy(&b.mu);
+}

@@ -44,6 +44,11 @@ uint32_t opoa_nrows(const opoa_t *g);   /* graph nodes after opoa_end */
 size_t ocsx_zmw(opoa_t *g, int mode, const char *seqs, const uint32_t *offs,
                 const uint32_t *lens, uint32_t n, char *out);
 
+/* Many ZMWs on nthreads CPU threads (kt_for semantics); out[i] capacity
+ * >= sum(lens[i]) + 1; cells[i] = DP cells of ZMW i. */
+void ocsx_batch(int mode, int nthreads, uint32_t nz, const char **seqs, const uint32_t **offs,
+                const uint32_t **lens, const uint32_t *nseg, char **out, size_t *olen, uint64_t *cells);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,90 @@
+"""GPU (HIP, through the C-ABI) vs oracle (C restatement): bit-exact CCS.
+
+The bar is byte equality of every CCS string (SPEC.md is integer-only, so no
+tolerance).  Sizes are chosen so the oracle finishes in seconds; the full
+BASELINE sizes are covered by test_gpu_full_size_properties.
+"""
+import pytest
+
+import ccsx_amd as cx
+from oracle.oracle import Poa, batch
+from tests.zmw_cases import edge_cases, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(engine, zs, mode, threads=8):
+    want, _, _ = batch(zs, mode, threads)
+    got = engine.run(zs, mode)
+    for i, (w, (g, status, cells)) in enumerate(zip(want, got)):
+        assert status == 0, f"ZMW {i}: device status {status}"
+        assert g == w, f"ZMW {i}: GPU CCS ({len(g)} bp) != oracle CCS ({len(w)} bp)"
+    return got
+
+
+@pytest.mark.parametrize("L,passes,n", [(2000, 8, 32), (10000, 8, 8), (2000, 30, 6), (5000, 12, 6)])
+def test_shredded_synthetic(engine, L, passes, n):
+    zs = [synth(h, L, passes) for h in range(n)]
+    _check(engine, zs, cx.MODE_SHRED)
+
+
+@pytest.mark.parametrize("L,passes,n", [(3000, 5, 16), (20000, 5, 2)])
+def test_primitive_synthetic(engine, L, passes, n):
+    zs = [synth(1000 + h, L, passes) for h in range(n)]
+    _check(engine, zs, cx.MODE_PRIMITIVE)
+
+
+@pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
+def test_edge_cases(engine, mode):
+    cases = edge_cases()
+    names = list(cases)
+    zs = [cases[k] for k in names]
+    want, _, _ = batch(zs, mode, 8)
+    got = engine.run(zs, mode)
+    for name, w, (g, status, _) in zip(names, want, got):
+        assert status == 0, f"{name}: device status {status}"
+        assert g == w, f"{name}: GPU CCS != oracle CCS"
+
+
+def test_cells_match_oracle(engine):
+    zs = [synth(h, 2000, 8) for h in range(4)]
+    _, cells, _ = batch(zs, cx.MODE_SHRED, 4)
+    got = engine.run(zs, cx.MODE_SHRED)
+    assert [c for _, _, c in got] == cells
+
+
+def test_mixed_batch_order_preserved(engine):
+    """Heterogeneous ZMWs in one launch come back in input order (main.c:707-717)."""
+    zs = [synth(h, L, p) for h, (L, p) in enumerate([(2000, 8), (6000, 5), (1500, 20), (9000, 6), (2500, 7)])]
+    _check(engine, zs, cx.MODE_SHRED)
+
+
+def test_repeat_launch_deterministic(engine):
+    zs = [synth(h, 3000, 8) for h in range(8)]
+    engine.stage(zs)
+    engine.launch(cx.MODE_SHRED)
+    a = engine.fetch()
+    engine.launch(cx.MODE_SHRED)
+    b = engine.fetch()
+    assert a == b
+
+
+def test_gpu_full_size_properties(engine):
+    """BASELINE config B shape (10 kb x 8) at a 64-ZMW sample: parity on a
+    subset plus size-independent properties on all (status, length, identity
+    to the synthetic truth)."""
+    import random
+    zs, truth = [], []
+    for h in range(64):
+        subs, ins = cx.synth_zmw(20201104, h, 10000, 8)
+        zs.append(cx.prepare(subs))
+        truth.append(ins)
+    got = engine.run(zs, cx.MODE_SHRED)
+    for (g, status, cells), ins in zip(got, truth):
+        assert status == 0
+        assert 9700 <= len(g) <= 10300
+        assert cells > 8_000_000
+    sample = random.Random(3).sample(range(64), 6)
+    want, _, _ = batch([zs[i] for i in sample], cx.MODE_SHRED, 6)
+    for i, w in zip(sample, want):
+        assert got[i][0] == w
