@@ -94,6 +94,13 @@ def build_product(verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
+    # diagnostic variant with per-phase DP stamps (tools/phase_prof.py --diag)
+    diag = os.path.join(HERE, "libccsx_amd_diag.so")
+    dobj = os.path.join(OBJ, "ccsx_kernel_diag.hip.o")
+    if _stale(dobj, [srcs[0]] + hdrs):
+        _run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS"] + common + ["-c", srcs[0], "-o", dobj])
+    if _stale(diag, objs[1:] + [dobj]):
+        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", diag, dobj] + objs[1:] + ["-lz", "-lpthread"])
     # the C host program
     main_src = os.path.join(CSRC, "host", "main.cpp")
     if os.path.exists(main_src) and _stale(BIN, [main_src, LIB] + hdrs):

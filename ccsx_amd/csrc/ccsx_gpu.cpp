@@ -61,6 +61,9 @@ struct ccsx_ctx {
     uint64_t seq_bytes = 0, ws_bytes = 0, out_bytes = 0, msa_bytes = 0;
     uint32_t nseg_total = 0;
     std::vector<ccsx::ZmwDesc> desc;
+    bool profiling = false;
+    DevBuf d_prof;
+    std::vector<unsigned long long> h_prof;
     DevBuf d_seq, d_soff, d_slen, d_desc, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
     // fetched results
     std::vector<uint8_t> h_out;
@@ -108,7 +111,7 @@ void ccsx_gpu_close(ccsx_ctx *c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    DevBuf *bufs[] = {&c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_ws, &c->d_out,
+    DevBuf *bufs[] = {&c->d_prof, &c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_ws, &c->d_out,
                       &c->d_msa, &c->d_olen, &c->d_ncols, &c->d_status, &c->d_cells};
     for (DevBuf *b : bufs) b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -249,7 +252,12 @@ int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
     a.nzmw = uint32_t(c->nz);
     a.lds_read_words = c->lds_read_words;
     a.lds_nmax = c->lds_nmax;
-    const uint32_t lds = uint32_t(ccsx::kRing * 260 * 4 + (c->lds_read_words + c->lds_nmax) * 4);
+    a.prof = nullptr;
+    if (c->profiling) {
+        HIPCHK(c, c->d_prof.reserve(c->nz * ccsx::kProfSlots * 8));
+        a.prof = c->d_prof.as<unsigned long long>();
+    }
+    const uint32_t lds = uint32_t((ccsx::kLdsFixedWords + c->lds_read_words + c->lds_nmax) * 4);
     if (lds > 160 * 1024) {
         c->err = "reads too long for the LDS read buffer";
         return -1;
@@ -313,6 +321,26 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     r = ccsx_gpu_launch(c, mode, nullptr);
     if (r) return r;
     return ccsx_gpu_fetch(c, out);
+}
+
+int ccsx_gpu_set_profiling(ccsx_ctx *c, int on)
+{
+    if (!c) return -1;
+    c->profiling = on != 0;
+    return 0;
+}
+
+int ccsx_gpu_profile(ccsx_ctx *c, uint64_t *sums, uint32_t nslots)
+{
+    if (!c || !c->profiling || nslots < (uint32_t)ccsx::kProfSlots) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    c->h_prof.assign(c->nz * ccsx::kProfSlots, 0);
+    if (c->nz)
+        HIPCHK(c, hipMemcpy(c->h_prof.data(), c->d_prof.p, c->nz * ccsx::kProfSlots * 8, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < nslots; ++i) sums[i] = 0;
+    for (size_t z = 0; z < c->nz; ++z)
+        for (int i = 0; i < ccsx::kProfSlots; ++i) sums[i] += c->h_prof[z * ccsx::kProfSlots + i];
+    return 0;
 }
 
 uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *c)

@@ -36,14 +36,26 @@ __device__ __forceinline__ int dpp(int old, int v)
     return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, BM, false);
 }
 
+// inclusive max-scan over the 64 lanes: six in-place DPP max ops (a lane
+// whose DPP source is out of range, or whose row is masked, is not written,
+// i.e. keeps its own value).  Hand-written because hipcc does not fold the
+// DPP movs into the max; the s_nop 1 cover the VALU-write -> DPP-read hazard.
 __device__ __forceinline__ int wave_incl_max(int v)
 {
-    v = max(v, dpp<0x111>(kNeg, v));
-    v = max(v, dpp<0x112>(kNeg, v));
-    v = max(v, dpp<0x114>(kNeg, v));
-    v = max(v, dpp<0x118>(kNeg, v));
-    v = max(v, dpp<0x142, 0xA>(kNeg, v));
-    v = max(v, dpp<0x143, 0xC>(kNeg, v));
+    asm("s_nop 1\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(v));
     return v;
 }
 
@@ -58,7 +70,9 @@ __device__ __forceinline__ int wave_incl_sum(int v)
     return v;
 }
 
-__device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old, v); }
+__device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old, v); }  // lane l <- l-1
+
+__device__ __forceinline__ int wave_shl1(int old, int v) { return dpp<0x130>(old, v); }  // lane l <- l+1
 
 __device__ __forceinline__ int wave_max(int v) { return __builtin_amdgcn_readlane(wave_incl_max(v), 63); }
 
@@ -99,9 +113,31 @@ struct Z {
     uint32_t rdcap;      // bases that fit in rd
     int cur;
     uint32_t R, E;
+    uint32_t slow;  // current graph has a predecessor > kRing rows back or a row with > 4 predecessors
     int32_t status;
     unsigned long long cells;
+    unsigned long long pf[kProfSlots];
 };
+
+__device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
+
+// Diagnostic build only (-DCCSX_DP_STAMPS, libccsx_amd_diag.so): shader-clock
+// stamps between the phases of one DP row; never compiled into the product.
+#ifdef CCSX_DP_STAMPS
+#define DP_STAMP(slot)                                                                      \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        unsigned long long t_;                                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        z.pf[slot] += t_ - t_prev;                                                          \
+        t_prev = t_;                                                                        \
+    } while (0)
+#else
+#define DP_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
 
 template <class T>
 __device__ __forceinline__ T *P(const Z &z, uint64_t off)
@@ -109,12 +145,18 @@ __device__ __forceinline__ T *P(const Z &z, uint64_t off)
     return reinterpret_cast<T *>(z.ws + off);
 }
 
+// graph buffer b (0/1) of the double-buffered rebuild (SPEC.md §5)
+__device__ __forceinline__ uint8_t *G_nb(const Z &z, int b) { return P<uint8_t>(z, b ? z.L.nb1 : z.L.nb0); }
+__device__ __forceinline__ uint64_t *G_mem(const Z &z, int b) { return P<uint64_t>(z, b ? z.L.mem1 : z.L.mem0); }
+__device__ __forceinline__ uint32_t *G_poff(const Z &z, int b) { return P<uint32_t>(z, b ? z.L.poff1 : z.L.poff0); }
+__device__ __forceinline__ uint32_t *G_pred(const Z &z, int b) { return P<uint32_t>(z, b ? z.L.pred1 : z.L.pred0); }
+
 __device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return (z.rd[j >> 4] >> ((j & 15u) * 2u)) & 3u; }
 
 // ----------------------------------------------------------------------------
 // push: stage read k (ASCII in HBM) into LDS as 2-bit codes
 // ----------------------------------------------------------------------------
-__device__ void load_read(Z &z, const uint8_t *src, uint32_t m)
+__device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
 {
     const uint32_t lane = threadIdx.x;
     const uint32_t nwd = (m + 15) / 16;
@@ -127,28 +169,6 @@ __device__ void load_read(Z &z, const uint8_t *src, uint32_t m)
             x |= c << (2 * b);
         }
         z.rd[w] = x;
-    }
-    __syncthreads();
-}
-
-// ----------------------------------------------------------------------------
-// SPEC.md §3: pre-pass -- which rows must be spilled (a successor further than
-// kRing rows away reads them after their LDS slot is reused)
-// ----------------------------------------------------------------------------
-__device__ void mark_spills(Z &z)
-{
-    const uint32_t lane = threadIdx.x;
-    uint8_t *spf = P<uint8_t>(z, z.L.spf);
-    const uint32_t *poff = P<uint32_t>(z, z.L.poff[z.cur]);
-    const uint32_t *pred = P<uint32_t>(z, z.L.pred[z.cur]);
-    for (uint32_t r = lane; r < z.R; r += 64) spf[r] = 0;
-    __syncthreads();
-    for (uint32_t s = lane; s < z.R; s += 64) {
-        const uint32_t e1 = poff[s + 1];
-        for (uint32_t e = poff[s]; e < e1; ++e) {
-            const uint32_t p = pred[e];
-            if (s - p > (uint32_t)kRing) spf[p] = 1;
-        }
     }
     __syncthreads();
 }
@@ -168,125 +188,229 @@ __device__ __forceinline__ int cell_glb(const int32_t *row, int c, int lane)
 {
     const int i = 2 * lane + c;
     if ((unsigned)i >= (unsigned)kW) return kNeg;
-    return row[(ARR + (i & 1)) * 64 + (i >> 1)];
+    return __builtin_nontemporal_load(row + (ARR + (i & 1)) * 64 + (i >> 1));
 }
 
 struct PredRow {
     int32_t off, rmax, rarg;
 };
 
+// LDS layout of one wave (int32 words)
+constexpr int kLdsRing = 0;                          // kRing rows x [Hev|Hod|Dev|Dod] x 64
+constexpr int kLdsMeta = kRing * 256;                // kRing x {off, rmax, rarg, -}
+constexpr int kLdsStCodes = kLdsMeta + kRing * 4;    // kBlk rows x 64 B of codes
+constexpr int kBlk = 16;                             // rows per flush block
+constexpr int kLdsStMeta = kLdsStCodes + kBlk * 16;  // kBlk x {off, mi}
+constexpr int kLdsStSlots = kLdsStMeta + kBlk * 2;   // kBlk x 256 B of slots
+constexpr int kLdsFixed = kLdsStSlots + kBlk * 64;   // then: packed read codes, shredding cursors
+static_assert(kBlk == kRing, "the ring doubles as the spill source of a flushed block");
+static_assert(kLdsFixed == kLdsFixedWords, "host and device LDS layouts disagree");
+
 __device__ __forceinline__ PredRow pred_meta(const Z &z, uint32_t r, uint32_t p)
 {
     PredRow m;
     if (r - p <= (uint32_t)kRing) {
-        const int32_t *mt = z.meta + (p % kRing) * 4;
+        const int32_t *mt = z.lds + kLdsMeta + (p % kRing) * 4;
         m.off = mt[0], m.rmax = mt[1], m.rarg = mt[2];
     } else {
-        m.off = P<int32_t>(z, z.L.roff)[p];
-        m.rmax = P<int32_t>(z, z.L.rmx)[p];
-        m.rarg = P<int32_t>(z, z.L.rag)[p];
+        const uint32_t sl = uni(__builtin_nontemporal_load(P<uint32_t>(z, z.L.sslot) + p));
+        const int32_t *rec = reinterpret_cast<const int32_t *>(z.ws + z.L.spill + (size_t)sl * (kW * 8 + 16));
+        m.off = uni(__builtin_nontemporal_load(rec + 256));
+        m.rmax = uni(__builtin_nontemporal_load(rec + 257));
+        m.rarg = uni(__builtin_nontemporal_load(rec + 258));
     }
     return m;
+}
+
+// Register set of one flush.  Two sets alternate (even/odd blocks) and each
+// is pinned live until it is rewritten two blocks later, so the global stores
+// of a flush never stall the DP on a store-data (WAR) wait.
+struct FlushBuf {
+    uint4 code;
+    uint2 meta;
+    uint4 slot[4];
+};
+
+__device__ __forceinline__ void pin(FlushBuf &f)
+{
+    asm volatile("" : "+v"(f.code.x), "+v"(f.code.y), "+v"(f.code.z), "+v"(f.code.w), "+v"(f.meta.x), "+v"(f.meta.y));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(f.slot[i].x), "+v"(f.slot[i].y), "+v"(f.slot[i].z), "+v"(f.slot[i].w));
 }
 
 // ----------------------------------------------------------------------------
 // SPEC.md §3: banded read-vs-graph DP for one read (codes in z.rd, length m)
 // ----------------------------------------------------------------------------
-__device__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
+// per lane: row r0+lane's base | spill flag << 2 | npred << 8, poff, first 4 predecessors
+struct RowPre {
+    uint32_t info, po, p0, p1, p2, p3;
+};
+
+struct DpState {
+    int32_t bE;
+    uint32_t bR, bJ;
+    uint32_t nmulti, nspill;
+    int32_t pH0, pH1, pD0, pD1, pOff, pRm, pRarg;  // row r-1 (registers)
+    RowPre cur, nxt;  // rows of the current / next 64-row superblock (one row per lane)
+};
+
+__device__ __forceinline__ void prefetch_rows(const Z &z, uint32_t r0, RowPre &o)
+{
+    const uint32_t rr = r0 + threadIdx.x;
+    if (rr < z.R) {
+        const uint8_t *nb = G_nb(z, z.cur);
+        const uint32_t *poff = G_poff(z, z.cur);
+        const uint32_t *pred = G_pred(z, z.cur);
+        o.po = poff[rr];
+        const uint32_t np = poff[rr + 1] - o.po;
+        o.p0 = np > 0 ? pred[o.po] : 0u;
+        o.p1 = np > 1 ? pred[o.po + 1] : 0u;
+        o.p2 = np > 2 ? pred[o.po + 2] : 0u;
+        o.p3 = np > 3 ? pred[o.po + 3] : 0u;
+        o.info = ((uint32_t)nb[rr] & 3u) | ((uint32_t)P<uint8_t>(z, z.L.spf)[rr] << 2) | (np << 8);
+    }
+}
+
+// one 16-row block of the DP, then its flush through register set f.
+// SLOW: some predecessor is further back than the LDS ring (spilled rows in
+// HBM) or has > 4 predecessors; otherwise the row loop never touches HBM.
+template <bool SLOW>
+__device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_t m, FlushBuf &f)
 {
     const int lane = threadIdx.x;
     const uint32_t R = z.R;
-    const uint8_t *nb = P<uint8_t>(z, z.L.nb[z.cur]);
-    const uint32_t *poff = P<uint32_t>(z, z.L.poff[z.cur]);
-    const uint32_t *pred = P<uint32_t>(z, z.L.pred[z.cur]);
-    const uint8_t *spf = P<uint8_t>(z, z.L.spf);
-    int32_t *g_roff = P<int32_t>(z, z.L.roff);
-    int32_t *g_rmx = P<int32_t>(z, z.L.rmx);
-    int32_t *g_rag = P<int32_t>(z, z.L.rag);
-    uint32_t *g_tof = P<uint32_t>(z, z.L.tof);
-    uint32_t *g_sslot = P<uint32_t>(z, z.L.sslot);
-    uint8_t *trace = P<uint8_t>(z, z.L.trace);
-    int32_t *spill = P<int32_t>(z, z.L.spill);
+    const uint32_t r0 = blk * kBlk;
+    if (r0 >= R) return;
+    const uint32_t *pred = G_pred(z, z.cur);
     const int32_t lim = m > (uint32_t)kW ? (int32_t)(m - kW) : 0;
     const int t0 = 2 * lane, t1 = 2 * lane + 1;
-
-    int32_t bE = INT32_MIN;
-    uint32_t bR = 0, bJ = 0;
-    uint32_t nmulti = 0, nspill = 0;
-    uint32_t blk_nb = 0, blk_po = 0, blk_np = 0, blk_p0 = 0, blk_p1 = 0, blk_sp = 0;
-
-    for (uint32_t r = 0; r < R; ++r) {
-        if ((r & 63u) == 0) {
-            const uint32_t rr = r + lane;
-            if (rr < R) {
-                blk_nb = nb[rr];
-                blk_po = poff[rr];
-                blk_np = poff[rr + 1] - blk_po;
-                blk_p0 = blk_np > 0 ? pred[blk_po] : 0u;
-                blk_p1 = blk_np > 1 ? pred[blk_po + 1] : 0u;
-                blk_sp = spf[rr];
-            }
-        }
+    int32_t *st_meta = z.lds + kLdsStMeta;
+    uint8_t *st_codes = reinterpret_cast<uint8_t *>(z.lds + kLdsStCodes);
+    uint32_t *st_slots = reinterpret_cast<uint32_t *>(z.lds + kLdsStSlots);
+    const uint32_t mi0 = S.nmulti;
+    if ((blk & 3u) == 0) {
+        if (blk == 0) prefetch_rows(z, 0, S.cur);
+        else S.cur = S.nxt;
+    } else if ((blk & 3u) == 1) {
+        // issue the next superblock's loads now; consumed 3 blocks later
+        prefetch_rows(z, (blk + 3) * kBlk, S.nxt);
+    }
+    const uint32_t rend = r0 + kBlk < R ? r0 + kBlk : R;
+    uint32_t spill_mask = 0;
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
+    for (uint32_t r = r0; r < rend; ++r) {
+        DP_STAMP(kPfRowE);
         const int li = (int)(r & 63u);
-        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)blk_nb, li) & 3u;
-        const uint32_t po = (uint32_t)__builtin_amdgcn_readlane((int)blk_po, li);
-        const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)blk_np, li);
-        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)blk_p0, li);
-        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)blk_p1, li);
-        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)blk_sp, li);
+        const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.info, li);
+        const uint32_t base = info & 3u, sp = (info >> 2) & 1u, np = info >> 8;
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p0, li);
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p1, li);
+        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p2, li);
+        const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p3, li);
+        const uint32_t po = SLOW ? (uint32_t)__builtin_amdgcn_readlane((int)S.cur.po, li) : 0u;
         if (np > 255u) {
             z.status = kErrInDegree;
             return;
         }
-        // band placement (SPEC.md §3.1)
+        auto predp = [&](uint32_t s) -> uint32_t {
+            if (s == 0) return p0;
+            if (s == 1) return p1;
+            if (s == 2) return p2;
+            if (s == 3 || !SLOW) return p3;
+            return uni(pred[po + s]);
+        };
+        // band placement (SPEC.md §3.1).  Common case -- the only predecessor
+        // is row r-1 -- from registers; otherwise from the LDS ring meta
+        // (row r-1 included) or, in SLOW mode, a spilled row's record.
+        auto meta = [&](uint32_t p) -> PredRow {
+            if (!SLOW || r - p <= (uint32_t)kRing) {
+                const int32_t *mt = z.lds + kLdsMeta + (p % kRing) * 4;
+                return PredRow{mt[0], mt[1], mt[2]};
+            }
+            return pred_meta(z, r, p);
+        };
+        const bool chain = np == 1 && p0 + 1 == r;
         int32_t off = 0;
-        if (np) {
-            int32_t bm = INT32_MIN, barg = 0;
-            for (uint32_t s = 0; s < np; ++s) {
-                const uint32_t p = s == 0 ? p0 : s == 1 ? p1 : uni(pred[po + s]);
-                const PredRow pm = pred_meta(z, r, p);
+        if (chain) {
+            off = S.pRarg + 1 - kW / 2;
+        } else if (np) {
+            const PredRow m0 = meta(p0);
+            int32_t bm = m0.rmax, barg = m0.rarg;
+            for (uint32_t s = 1; s < np; ++s) {
+                const PredRow pm = meta(predp(s));
                 if (pm.rmax > bm) bm = pm.rmax, barg = pm.rarg;
             }
             off = barg + 1 - kW / 2;
-            off = off < 0 ? 0 : off;
-            off = off > lim ? lim : off;
         }
+        off = off < 0 ? 0 : off;
+        off = off > lim ? lim : off;
+        DP_STAMP(kPfRowA);
         // predecessor terms (SPEC.md §3.2)
         int32_t Mh0 = kNeg, Mh1 = kNeg, Dv0 = kNeg, Dv1 = kNeg;
         uint32_t ms0 = 0, ms1 = 0, ds0 = 0, ds1 = 0, dx0 = 0, dx1 = 0;
-        for (uint32_t s = 0; s < np; ++s) {
-            const uint32_t p = s == 0 ? p0 : s == 1 ? p1 : uni(pred[po + s]);
-            const PredRow pm = pred_meta(z, r, p);
-            const int sh = off - pm.off;
+        const int32_t sh1 = off - S.pOff;
+        if (chain && (uint32_t)sh1 <= 2u) {
+            // fast path: the only predecessor is the previous row, band shift
+            // 0..2 -> its cells come from registers through DPP lane shifts
             int hA, hB, hC, dB, dC;
-            if (r - p <= (uint32_t)kRing) {
-                const int32_t *row = z.lds + (p % kRing) * 256;
-                hA = cell_lds<0>(row, sh - 1, lane);
-                hB = cell_lds<0>(row, sh, lane);
-                hC = cell_lds<0>(row, sh + 1, lane);
-                dB = cell_lds<2>(row, sh, lane);
-                dC = cell_lds<2>(row, sh + 1, lane);
+            if (sh1 == 0) {
+                hA = wave_shr1(kNeg, S.pH1), hB = S.pH0, hC = S.pH1, dB = S.pD0, dC = S.pD1;
+            } else if (sh1 == 1) {
+                hA = S.pH0, hB = S.pH1, hC = wave_shl1(kNeg, S.pH0), dB = S.pD1, dC = wave_shl1(kNeg, S.pD0);
             } else {
-                const int32_t *row = spill + (size_t)g_sslot[p] * 256;
-                hA = cell_glb<0>(row, sh - 1, lane);
-                hB = cell_glb<0>(row, sh, lane);
-                hC = cell_glb<0>(row, sh + 1, lane);
-                dB = cell_glb<2>(row, sh, lane);
-                dC = cell_glb<2>(row, sh + 1, lane);
+                hA = S.pH1, hB = wave_shl1(kNeg, S.pH0), hC = wave_shl1(kNeg, S.pH1);
+                dB = wave_shl1(kNeg, S.pD0), dC = wave_shl1(kNeg, S.pD1);
             }
-            if (hA > Mh0) Mh0 = hA, ms0 = s;
-            if (hB > Mh1) Mh1 = hB, ms1 = s;
+            Mh0 = hA, Mh1 = hB;
             {
                 const int a = hB + kO + kE, b = dB + kE;
                 const int c = b > a ? b : a;
-                if (c > Dv0) Dv0 = c, ds0 = s, dx0 = b > a;
+                if (c > kNeg) Dv0 = c, dx0 = b > a;
             }
             {
                 const int a = hC + kO + kE, b = dC + kE;
                 const int c = b > a ? b : a;
-                if (c > Dv1) Dv1 = c, ds1 = s, dx1 = b > a;
+                if (c > kNeg) Dv1 = c, dx1 = b > a;
+            }
+        } else {
+            for (uint32_t s = 0; s < np; ++s) {
+                const uint32_t p = predp(s);
+                const PredRow pm = meta(p);
+                const int sh = off - pm.off;
+                int hA, hB, hC, dB, dC;
+                if (!SLOW || r - p <= (uint32_t)kRing) {
+                    const int32_t *row = z.lds + kLdsRing + (p % kRing) * 256;
+                    hA = cell_lds<0>(row, sh - 1, lane);
+                    hB = cell_lds<0>(row, sh, lane);
+                    hC = cell_lds<0>(row, sh + 1, lane);
+                    dB = cell_lds<2>(row, sh, lane);
+                    dC = cell_lds<2>(row, sh + 1, lane);
+                } else {
+                    const uint32_t sl = uni(__builtin_nontemporal_load(P<uint32_t>(z, z.L.sslot) + p));
+                    const int32_t *row = reinterpret_cast<const int32_t *>(z.ws + z.L.spill + (size_t)sl * (kW * 8 + 16));
+                    hA = cell_glb<0>(row, sh - 1, lane);
+                    hB = cell_glb<0>(row, sh, lane);
+                    hC = cell_glb<0>(row, sh + 1, lane);
+                    dB = cell_glb<2>(row, sh, lane);
+                    dC = cell_glb<2>(row, sh + 1, lane);
+                }
+                if (hA > Mh0) Mh0 = hA, ms0 = s;
+                if (hB > Mh1) Mh1 = hB, ms1 = s;
+                {
+                    const int a = hB + kO + kE, b = dB + kE;
+                    const int c = b > a ? b : a;
+                    if (c > Dv0) Dv0 = c, ds0 = s, dx0 = b > a;
+                }
+                {
+                    const int a = hC + kO + kE, b = dC + kE;
+                    const int c = b > a ? b : a;
+                    if (c > Dv1) Dv1 = c, ds1 = s, dx1 = b > a;
+                }
             }
         }
+        DP_STAMP(kPfRowB);
         const int32_t j0 = off + t0, j1 = off + t1;
         const bool v0 = j0 < (int32_t)m, v1 = j1 < (int32_t)m;
         const uint32_t q0 = v0 ? rcode(z, (uint32_t)j0) : 0u;
@@ -319,115 +443,243 @@ __device__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
         uint32_t c1 = hc1 | (dx1 << 2) | (iext1 << 3);
         if (!v0) H0 = kNeg, Dv0 = kNeg, c0 = 0, ms0 = 0, ds0 = 0;
         if (!v1) H1 = kNeg, Dv1 = kNeg, c1 = 0, ms1 = 0, ds1 = 0;
+        DP_STAMP(kPfRowC);
         // row max / argmax for the successors' band placement
         const int32_t rm = wave_max(max(H0, H1));
-        const uint64_t hit = ballot(H0 == rm || H1 == rm);
-        const int L = (int)__builtin_ctzll(hit);
-        const int32_t hL = __builtin_amdgcn_readlane(H0, L);
-        const int32_t rarg = off + 2 * L + (hL == rm ? 0 : 1);
+        const uint64_t hit0 = ballot(H0 == rm), hit1 = ballot(H1 == rm);
+        const uint32_t c0i = hit0 ? 2u * (uint32_t)__builtin_ctzll(hit0) : 256u;
+        const uint32_t c1i = hit1 ? 2u * (uint32_t)__builtin_ctzll(hit1) + 1u : 256u;
+        const int32_t rarg = off + (int32_t)(c0i < c1i ? c0i : c1i);
         // free-end candidates (SPEC.md §3.5)
         if (v0) {
             const int32_t e = H0 + (j0 == (int32_t)m - 1 ? 0 : kO + kE * ((int32_t)m - 1 - j0));
-            if (e > bE) bE = e, bR = r, bJ = (uint32_t)j0;
+            if (e > S.bE) S.bE = e, S.bR = r, S.bJ = (uint32_t)j0;
         }
         if (v1) {
             const int32_t e = H1 + (j1 == (int32_t)m - 1 ? 0 : kO + kE * ((int32_t)m - 1 - j1));
-            if (e > bE) bE = e, bR = r, bJ = (uint32_t)j1;
+            if (e > S.bE) S.bE = e, S.bR = r, S.bJ = (uint32_t)j1;
         }
-        // traceback codes: 64 B per row (+256 B of predecessor slots if np > 1)
-        const uint32_t tof = r * 64u + nmulti * 256u;
-        trace[tof + lane] = (uint8_t)(c0 | (c1 << 4));
+        DP_STAMP(kPfRowD);
+        // staged in LDS, flushed to HBM once per block
+        const uint32_t i = r - r0;
+        st_codes[i * 64 + lane] = (uint8_t)(c0 | (c1 << 4));
+        uint32_t mi = kNone;
         if (np > 1) {
-            if (nmulti >= z.d.mcap) {
-                z.status = kErrMulti;
-                return;
-            }
-            reinterpret_cast<uint32_t *>(trace + tof + 64)[lane] = ms0 | (ms1 << 8) | (ds0 << 16) | (ds1 << 24);
-            ++nmulti;
+            mi = S.nmulti - mi0;
+            st_slots[mi * 64 + lane] = ms0 | (ms1 << 8) | (ds0 << 16) | (ds1 << 24);
+            mi = S.nmulti++;
         }
-        // the row itself: LDS ring (+ HBM spill) and its meta
-        int32_t *row = z.lds + (r % kRing) * 256;
+        if (lane == 0) {
+            st_meta[i * 2] = off;
+            st_meta[i * 2 + 1] = (int32_t)mi;
+        }
+        int32_t *row = z.lds + kLdsRing + (r % kRing) * 256;
         row[lane] = H0;
         row[64 + lane] = H1;
         row[128 + lane] = Dv0;
         row[192 + lane] = Dv1;
         if (lane == 0) {
-            int32_t *mt = z.meta + (r % kRing) * 4;
+            int32_t *mt = z.lds + kLdsMeta + (r % kRing) * 4;
             mt[0] = off, mt[1] = rm, mt[2] = rarg;
-            g_roff[r] = off;
-            g_rmx[r] = rm;
-            g_rag[r] = rarg;
-            g_tof[r] = tof;
         }
-        if (sp) {
-            if (nspill >= z.d.scap) {
-                z.status = kErrSpill;
-                return;
-            }
-            int32_t *srow = spill + (size_t)nspill * 256;
-            srow[lane] = H0;
-            srow[64 + lane] = H1;
-            srow[128 + lane] = Dv0;
-            srow[192 + lane] = Dv1;
-            if (lane == 0) g_sslot[r] = nspill;
-            ++nspill;
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): ring row visible to the next row
-        __builtin_amdgcn_wave_barrier();
+        spill_mask |= sp << i;
+        S.pH0 = H0, S.pH1 = H1, S.pD0 = Dv0, S.pD1 = Dv1, S.pOff = off, S.pRm = rm, S.pRarg = rarg;
     }
+    DP_STAMP(kPfRowE);
+    const uint32_t nm = S.nmulti - mi0;
+    if (S.nmulti > z.d.mcap) {
+        z.status = kErrMulti;
+        return;
+    }
+    // flush: codes (64 B/row), row meta, multi slots; registers f stay pinned
+    pin(f);
+    const uint32_t nrow = rend - r0;
+    uint8_t *codes = z.ws + z.L.codes + (size_t)r0 * 64;
+    uint2 *rmeta = reinterpret_cast<uint2 *>(z.ws + z.L.rmeta) + r0;
+    uint8_t *slots = z.ws + z.L.slots + (size_t)mi0 * 256;
+    f.code = reinterpret_cast<const uint4 *>(st_codes)[lane];
+    if ((uint32_t)lane * 16 < nrow * 64) reinterpret_cast<uint4 *>(codes)[lane] = f.code;
+    f.meta = reinterpret_cast<const uint2 *>(st_meta)[lane & (kBlk - 1)];
+    if ((uint32_t)lane < nrow) rmeta[lane] = f.meta;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t chunk = (uint32_t)lane + 64u * c;
+        f.slot[c] = reinterpret_cast<const uint4 *>(st_slots)[chunk];
+        if (chunk * 16 < nm * 256) reinterpret_cast<uint4 *>(slots)[chunk] = f.slot[c];
+    }
+    // rows needed beyond the ring: copy them (still in the ring) to HBM
+    while (SLOW && spill_mask) {
+        const uint32_t i = __builtin_ctz(spill_mask);
+        spill_mask &= spill_mask - 1;
+        const uint32_t r = r0 + i;
+        if (S.nspill >= z.d.scap) {
+            z.status = kErrSpill;
+            return;
+        }
+        int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)S.nspill * (kW * 8 + 16));
+        const int32_t *row = z.lds + kLdsRing + (r % kRing) * 256;
+        const int32_t *mt = z.lds + kLdsMeta + (r % kRing) * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rec[q * 64 + lane] = row[q * 64 + lane];
+        if (lane < 3) rec[256 + lane] = mt[lane];
+        if (lane == 0) P<uint32_t>(z, z.L.sslot)[r] = S.nspill;
+        ++S.nspill;
+    }
+}
+
+__device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
+{
+    DpState S;
+    S.bE = INT32_MIN, S.bR = 0, S.bJ = 0, S.nmulti = 0, S.nspill = 0;
+    S.pH0 = S.pH1 = S.pD0 = S.pD1 = kNeg, S.pOff = 0, S.pRm = 0, S.pRarg = 0;
+    S.cur = RowPre{0, 0, 0, 0, 0, 0};
+    S.nxt = S.cur;
+    FlushBuf fa, fb;
+    fa.code = fb.code = make_uint4(0, 0, 0, 0);
+    fa.meta = fb.meta = make_uint2(0, 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) fa.slot[c] = fb.slot[c] = make_uint4(0, 0, 0, 0);
+    const uint32_t nblk = (z.R + kBlk - 1) / kBlk;
+    if (z.slow) {
+        for (uint32_t blk = 0; blk < nblk && !z.status; blk += 2) {
+            dp_block<true>(z, S, blk, m, fa);
+            if (z.status) break;
+            dp_block<true>(z, S, blk + 1, m, fb);
+        }
+    } else {
+        for (uint32_t blk = 0; blk < nblk && !z.status; blk += 2) {
+            dp_block<false>(z, S, blk, m, fa);
+            if (z.status) break;
+            dp_block<false>(z, S, blk + 1, m, fb);
+        }
+    }
+    pin(fa);
+    pin(fb);
     // lexicographic (max score, min row, min j) over the lanes' candidates
-    const int32_t best = wave_max(bE);
-    const uint32_t rsel = bE == best ? bR : 0x7FFFFFFFu;
+    const int32_t best = wave_max(S.bE);
+    const uint32_t rsel = S.bE == best ? S.bR : 0x7FFFFFFFu;
     const int32_t rmin = wave_min((int32_t)rsel);
-    const uint32_t jsel = (bE == best && bR == (uint32_t)rmin) ? bJ : 0x7FFFFFFFu;
+    const uint32_t jsel = (S.bE == best && S.bR == (uint32_t)rmin) ? S.bJ : 0x7FFFFFFFu;
     const int32_t jmin = wave_min((int32_t)jsel);
     er_out = (uint32_t)rmin;
     ej_out = (uint32_t)jmin;
-    z.cells += (unsigned long long)R * (m < (uint32_t)kW ? m : (uint32_t)kW);
+    z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
     __syncthreads();
 }
 
 // ----------------------------------------------------------------------------
-// SPEC.md §4: traceback into one event per read base (lane 0 walks)
+// SPEC.md §4: traceback into one event per read base.  The path walks rows
+// backwards; blocks of kTbRows rows (band offsets, first two predecessors,
+// their code rows and the slots of their multi-predecessor rows) are staged
+// into LDS by the whole wave, then lane 0 walks inside LDS.
 // ----------------------------------------------------------------------------
-__device__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
+constexpr uint32_t kTbRows = 32;
+
+__device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
     const uint32_t lane = threadIdx.x;
     uint32_t *ev = P<uint32_t>(z, z.L.ev);
     for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
-    const uint32_t *poff = P<uint32_t>(z, z.L.poff[z.cur]);
-    const uint32_t *pred = P<uint32_t>(z, z.L.pred[z.cur]);
-    const int32_t *g_roff = P<int32_t>(z, z.L.roff);
-    const uint32_t *g_tof = P<uint32_t>(z, z.L.tof);
-    const uint8_t *trace = P<uint8_t>(z, z.L.trace);
-    uint32_t lead_row = 0, lead_j = 0;
-    int32_t err = 0;
-    if (lane == 0) {
-        uint32_t r = er;
-        int32_t j = (int32_t)ej;
-        int st = 0;
-        uint64_t guard = 0;
-        const uint64_t lim = (uint64_t)z.R * 2 + (uint64_t)m * 2 + 16;
-        for (;;) {
-            if (++guard > lim) {
+    const uint32_t *poff = G_poff(z, z.cur);
+    const uint32_t *pred = G_pred(z, z.cur);
+    const uint2 *rmeta = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta);
+    const uint8_t *codes = z.ws + z.L.codes;
+    const uint8_t *slots = z.ws + z.L.slots;
+    int32_t *tbm = z.lds;                                                 // [kTbRows][4]: roff, mi-rel, p0, p1
+    uint32_t *tbpo = reinterpret_cast<uint32_t *>(z.lds + 4 * kTbRows);   // [kTbRows]: poff
+    uint32_t *tbnp = reinterpret_cast<uint32_t *>(z.lds + 5 * kTbRows);   // [kTbRows]: #predecessors
+    uint8_t *tbc = reinterpret_cast<uint8_t *>(z.lds + 256);              // kTbRows x 64 B codes
+    uint8_t *tbs = reinterpret_cast<uint8_t *>(z.lds + 256 + 16 * kTbRows);  // slots of the block's multi rows
+    uint32_t *evs = reinterpret_cast<uint32_t *>(z.lds + 256 + 16 * kTbRows + 64 * kTbRows);  // walk output
+    constexpr uint32_t kEvStage = 2048;
+    static_assert(256 + 16 * kTbRows + 64 * kTbRows + kEvStage <= (uint32_t)kLdsFixedWords, "traceback LDS");
+    uint32_t r = er, lead_row = 0, lead_j = 0;
+    int32_t j = (int32_t)ej, st = 0, err = 0, done = 0;
+    uint64_t guard = 0;
+    const uint64_t glim = (uint64_t)z.R * 2 + (uint64_t)m * 2 + 16;
+    while (!done) {
+        const uint32_t blo = r >= kTbRows - 1 ? r - (kTbRows - 1) : 0u;
+        const uint32_t nr = r - blo + 1;
+        uint32_t mi = kNone;
+        if (lane < nr) {
+            const uint32_t row = blo + lane;
+            const uint32_t po = poff[row];
+            const uint32_t np = poff[row + 1] - po;
+            const uint2 mt = rmeta[row];
+            mi = mt.y;
+            tbm[lane * 4 + 0] = (int32_t)mt.x;
+            tbm[lane * 4 + 2] = np > 0 ? (int32_t)pred[po] : 0;
+            tbm[lane * 4 + 3] = np > 1 ? (int32_t)pred[po + 1] : 0;
+            tbpo[lane] = po;
+            tbnp[lane] = np;
+        }
+        // multi ordinals are increasing in row order: the block's slots are contiguous
+        const uint32_t mi_lo = (uint32_t)wave_min((int32_t)(mi == kNone ? 0x7FFFFFFFu : mi));
+        const uint32_t mi_hi = (uint32_t)wave_max((int32_t)(mi == kNone ? 0u : mi + 1));
+        const uint32_t nms = mi_lo == 0x7FFFFFFFu ? 0u : mi_hi - mi_lo;
+        if (lane < nr) tbm[lane * 4 + 1] = (int32_t)(mi == kNone ? kNone : mi - mi_lo);
+        for (uint32_t o = lane * 16; o < nr * 64; o += 1024)
+            *reinterpret_cast<uint4 *>(tbc + o) = *reinterpret_cast<const uint4 *>(codes + (size_t)blo * 64 + o);
+        for (uint32_t o = lane * 16; o < nms * 256; o += 1024)
+            *reinterpret_cast<uint4 *>(tbs + o) = *reinterpret_cast<const uint4 *>(slots + (size_t)mi_lo * 256 + o);
+        __syncthreads();
+        // The wave walks (uniform state).  Runs of diagonal steps -- MPRED on
+        // single-predecessor rows whose predecessor is the previous row, the
+        // bulk of any path -- are taken up to 64 at a time: lane i checks step
+        // i and a ballot finds the first break.  Other steps go one by one.
+        // Events go to LDS (a global store per step would stall the next step
+        // on its store-data wait) and are flushed by the wave.
+        const int32_t jhi = j;
+        uint32_t nev = 0;
+        while (r >= blo && nev + 64 <= kEvStage) {
+            if (++guard > glim) {
                 err = kErrTrace;
+                done = 1;
                 break;
             }
-            const uint32_t t = (uint32_t)(j - g_roff[r]);
-            const uint32_t tof = g_tof[r];
-            const uint32_t c = (trace[tof + (t >> 1)] >> ((t & 1u) * 4u)) & 15u;
+            if (st == 0) {
+                const int32_t rr = (int32_t)r - (int32_t)lane, jj = j - (int32_t)lane;
+                bool ok = rr >= (int32_t)blo && jj >= 1;
+                if (ok) {
+                    const uint32_t ri = (uint32_t)rr - blo;
+                    const int32_t *mt = tbm + ri * 4;
+                    const int32_t t = jj - mt[0];
+                    ok = t >= 0 && t < kW && tbnp[ri] == 1u && mt[2] == rr - 1;
+                    if (ok) ok = ((tbc[ri * 64 + (t >> 1)] >> ((t & 1) * 4)) & 3) == HC_MPRED;
+                }
+                const uint64_t bad = ~ballot(ok);
+                const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+                if (k) {
+                    if (lane < k) evs[nev + lane] = (EV_ALN << 30) | (uint32_t)rr;
+                    nev += k;
+                    r -= k;
+                    j -= (int32_t)k;
+                    continue;
+                }
+            }
+            const uint32_t ri = r - blo;
+            const int32_t roff = uni(tbm[ri * 4]);
+            const uint32_t mrel = (uint32_t)uni(tbm[ri * 4 + 1]);
+            const uint32_t rp0 = (uint32_t)uni(tbm[ri * 4 + 2]), rp1 = (uint32_t)uni(tbm[ri * 4 + 3]);
+            const uint32_t t = (uint32_t)(j - roff);
+            const uint32_t c = (uint32_t)uni((int)((tbc[ri * 64 + (t >> 1)] >> ((t & 1u) * 4u)) & 15u));
+            auto pred_of = [&](uint32_t s) -> uint32_t {
+                return s == 0 ? rp0 : s == 1 ? rp1 : uni(pred[uni(tbpo[ri]) + s]);
+            };
             if (st == 0) {
                 const uint32_t hc = c & 3u;
                 if (hc == HC_MPRED) {
-                    ev[j] = (EV_ALN << 30) | r;
-                    const uint32_t np = poff[r + 1] - poff[r];
-                    const uint32_t s = np > 1 ? trace[tof + 64 + (t >> 1) * 4 + (t & 1u)] : 0u;
-                    r = pred[poff[r] + s];
+                    if (lane == 0) evs[nev] = (EV_ALN << 30) | r;
+                    ++nev;
+                    const uint32_t s = mrel != kNone ? (uint32_t)uni((int)tbs[mrel * 256 + (t >> 1) * 4 + (t & 1u)]) : 0u;
+                    r = pred_of(s);
                     --j;
                 } else if (hc == HC_MSRC) {
-                    ev[j] = (EV_ALN << 30) | r;
+                    if (lane == 0) evs[nev] = (EV_ALN << 30) | r;
+                    ++nev;
                     lead_row = r;
                     lead_j = (uint32_t)j;
+                    done = 1;
                     break;
                 } else if (hc == HC_DEL) {
                     st = 1;
@@ -435,26 +687,27 @@ __device__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
                     st = 2;
                 }
             } else if (st == 1) {
-                const uint32_t np = poff[r + 1] - poff[r];
-                const uint32_t s = np > 1 ? trace[tof + 64 + (t >> 1) * 4 + 2 + (t & 1u)] : 0u;
+                const uint32_t s = mrel != kNone ? (uint32_t)uni((int)tbs[mrel * 256 + (t >> 1) * 4 + 2 + (t & 1u)]) : 0u;
                 st = (c >> 2) & 1u ? 1 : 0;
-                r = pred[poff[r] + s];
+                r = pred_of(s);
             } else {
-                ev[j] = (EV_INS << 30) | r;
+                if (lane == 0) evs[nev] = (EV_INS << 30) | r;
+                ++nev;
                 st = (c >> 3) & 1u ? 2 : 0;
                 --j;
             }
         }
+        nev = (uint32_t)__builtin_amdgcn_readfirstlane((int)nev);
+        for (uint32_t i = lane; i < nev; i += 64) ev[jhi - (int32_t)i] = evs[i];
+        __syncthreads();
     }
-    err = __builtin_amdgcn_readfirstlane(err);
     if (err) {
         z.status = err;
         return;
     }
     lead_row = uni(lead_row);
     lead_j = uni(lead_j);
-    __syncthreads();
-    for (uint32_t j = lane; j < lead_j; j += 64) ev[j] = (EV_LEAD << 30) | lead_row;
+    for (uint32_t jj = lane; jj < lead_j; jj += 64) ev[jj] = (EV_LEAD << 30) | lead_row;
     __syncthreads();
 }
 
@@ -474,19 +727,19 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
     return v;
 }
 
-__device__ void merge(Z &z, uint32_t k, uint32_t m)
+__device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
 {
     const uint32_t lane = threadIdx.x;
     const uint32_t R = z.R, nw = z.d.nw;
     const int a = z.cur, b = a ^ 1;
-    const uint8_t *nb = P<uint8_t>(z, z.L.nb[a]);
-    const uint64_t *mem = P<uint64_t>(z, z.L.mem[a]);
-    const uint32_t *poff = P<uint32_t>(z, z.L.poff[a]);
-    const uint32_t *pred = P<uint32_t>(z, z.L.pred[a]);
-    uint8_t *nb2 = P<uint8_t>(z, z.L.nb[b]);
-    uint64_t *mem2 = P<uint64_t>(z, z.L.mem[b]);
-    uint32_t *poff2 = P<uint32_t>(z, z.L.poff[b]);
-    uint32_t *pred2 = P<uint32_t>(z, z.L.pred[b]);
+    const uint8_t *nb = G_nb(z, a);
+    const uint64_t *mem = G_mem(z, a);
+    const uint32_t *poff = G_poff(z, a);
+    const uint32_t *pred = G_pred(z, a);
+    uint8_t *nb2 = G_nb(z, b);
+    uint64_t *mem2 = G_mem(z, b);
+    uint32_t *poff2 = G_poff(z, b);
+    uint32_t *pred2 = G_pred(z, b);
     const uint32_t *ev = P<uint32_t>(z, z.L.ev);
     uint32_t *tgt = P<uint32_t>(z, z.L.tgt);
     uint32_t *ipt = P<uint32_t>(z, z.L.ipt);
@@ -496,6 +749,7 @@ __device__ void merge(Z &z, uint32_t k, uint32_t m)
     uint8_t *fixf = P<uint8_t>(z, z.L.fixf);
     uint32_t *addp = P<uint32_t>(z, z.L.addp);
     uint32_t *cntn = P<uint32_t>(z, z.L.cntn);
+    uint8_t *spf = P<uint8_t>(z, z.L.spf);  // spill flags of the new graph (SPEC.md §3)
 
     // M1: classify every read base, number the new nodes in read order
     uint32_t K = 0;
@@ -597,12 +851,14 @@ __device__ void merge(Z &z, uint32_t k, uint32_t m)
     for (uint32_t x = lane; x < R; x += 64) {
         const uint32_t n = x + shift[x];
         nb2[n] = fixf[x] ? (uint8_t)(nb[x] & 3u) : nb[x];
+        spf[n] = 0;
         for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = mem[(size_t)x * nw + w];
         cntn[n] = poff[x + 1] - poff[x] + (addp[n] != kNone ? 1u : 0u);
     }
     for (uint32_t i = lane; i < K; i += 64) {
         const uint32_t n = ipt[i] + i;
         nb2[n] = iinf[i];
+        spf[n] = 0;
         for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = 0;
         cntn[n] = addp[n] != kNone ? 1u : 0u;
     }
@@ -629,20 +885,30 @@ __device__ void merge(Z &z, uint32_t k, uint32_t m)
         z.E = E2;
     }
     __syncthreads();
+    uint32_t slow = 0;
     for (uint32_t x = lane; x < R; x += 64) {
         const uint32_t n = x + shift[x];
         uint32_t o = poff2[n];
         const uint32_t e1 = poff[x + 1];
+        slow |= (e1 - poff[x] + (addp[n] != kNone ? 1u : 0u)) > 4u;
         for (uint32_t e = poff[x]; e < e1; ++e) {
-            const uint32_t p = pred[e];
-            pred2[o++] = p + shift[p];
+            const uint32_t p = pred[e] + shift[pred[e]];
+            pred2[o++] = p;
+            if (n - p > (uint32_t)kRing) spf[p] = 1, slow = 1;
         }
-        if (addp[n] != kNone) pred2[o] = addp[n];
+        if (addp[n] != kNone) {
+            pred2[o] = addp[n];
+            if (n - addp[n] > (uint32_t)kRing) spf[addp[n]] = 1, slow = 1;
+        }
     }
     for (uint32_t i = lane; i < K; i += 64) {
         const uint32_t n = ipt[i] + i;
-        if (addp[n] != kNone) pred2[poff2[n]] = addp[n];
+        if (addp[n] != kNone) {
+            pred2[poff2[n]] = addp[n];
+            if (n - addp[n] > (uint32_t)kRing) spf[addp[n]] = 1, slow = 1;
+        }
     }
+    z.slow = ballot(slow != 0) != 0;
     // M5: first/last rows of the reads
     uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
     for (uint32_t kk = lane; kk < k; kk += 64)
@@ -662,12 +928,12 @@ __device__ void merge(Z &z, uint32_t k, uint32_t m)
 // ----------------------------------------------------------------------------
 // SPEC.md §6: columns, per-column consensus and the consensus-match masks
 // ----------------------------------------------------------------------------
-__device__ uint32_t call_columns(Z &z, uint32_t n)
+__device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
 {
     const uint32_t lane = threadIdx.x;
     const uint32_t R = z.R, nw = z.d.nw;
-    const uint8_t *nb = P<uint8_t>(z, z.L.nb[z.cur]);
-    const uint64_t *mem = P<uint64_t>(z, z.L.mem[z.cur]);
+    const uint8_t *nb = G_nb(z, z.cur);
+    const uint64_t *mem = G_mem(z, z.cur);
     uint32_t *colof = P<uint32_t>(z, z.L.colof);
     uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
     uint8_t *cons = P<uint8_t>(z, z.L.cons);
@@ -720,14 +986,14 @@ __device__ uint32_t call_columns(Z &z, uint32_t n)
 // ----------------------------------------------------------------------------
 // end_bspoa over the reads staged in rdoff/rdlen (main.c:492,571)
 // ----------------------------------------------------------------------------
-__device__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zseq)
+__device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zseq)
 {
     const uint32_t *rdoff = P<uint32_t>(z, z.L.rdoff), *rdlen = P<uint32_t>(z, z.L.rdlen);
     uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
     z.R = 0;
     z.E = 0;
     z.cur = 0;
-    if (threadIdx.x == 0) P<uint32_t>(z, z.L.poff[0])[0] = 0;
+    if (threadIdx.x == 0) G_poff(z, 0)[0] = 0;
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t m = uni(rdlen[k]);
         if (threadIdx.x == 0) rfirst[k] = rlast[k] = kNone;
@@ -737,23 +1003,34 @@ __device__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zseq)
             z.status = kErrReadLen;
             return 0;
         }
+        unsigned long long t0 = stamp();
         load_read(z, zseq + uni(rdoff[k]), m);
+        unsigned long long t1 = stamp();
+        z.pf[kPfLoad] += t1 - t0;
         if (z.R) {
             uint32_t er, ej;
-            mark_spills(z);
+            z.pf[kPfRows] += z.R;
             dp_align(z, m, er, ej);
             if (z.status) return 0;
+            unsigned long long t2 = stamp();
+            z.pf[kPfDp] += t2 - t1;
             traceback(z, m, er, ej);
             if (z.status) return 0;
+            t1 = stamp();
+            z.pf[kPfTrace] += t1 - t2;
         }
         merge(z, k, m);
         if (z.status) return 0;
+        z.pf[kPfMerge] += stamp() - t1;
     }
-    return call_columns(z, n);
+    unsigned long long t3 = stamp();
+    const uint32_t nc = call_columns(z, n);
+    z.pf[kPfColumns] += stamp() - t3;
+    return nc;
 }
 
 // main.c:580-612: largest i >= 1 whose 10-column window is a clean breakpoint
-__device__ bool bp_ok(const Z &z, uint32_t i, uint32_t nseq, uint32_t colrate)
+__device__ __forceinline__ bool bp_ok(const Z &z, uint32_t i, uint32_t nseq, uint32_t colrate)
 {
     const uint32_t window = 10, minwin = 5, rowrate = 80, nw = z.d.nw;
     const uint8_t *cons = P<uint8_t>(z, z.L.cons);
@@ -779,7 +1056,7 @@ __device__ bool bp_ok(const Z &z, uint32_t i, uint32_t nseq, uint32_t colrate)
     return true;
 }
 
-__device__ uint32_t find_breakpoint(const Z &z, uint32_t ncols, uint32_t nseq, uint32_t colrate)
+__device__ __forceinline__ uint32_t find_breakpoint(const Z &z, uint32_t ncols, uint32_t nseq, uint32_t colrate)
 {
     const uint32_t window = 10;
     if (ncols <= window) return 0;  // SPEC.md §7 (main.c:580 would underflow)
@@ -793,13 +1070,13 @@ __device__ uint32_t find_breakpoint(const Z &z, uint32_t ncols, uint32_t nseq, u
 }
 
 // emit the consensus of columns [0, i) (main.c:622-638); advance pos if flag
-__device__ void emit(Z &z, uint32_t i, uint32_t ncols, uint32_t n, bool flag, uint8_t *out, uint32_t &ol)
+__device__ __forceinline__ void emit(Z &z, uint32_t i, uint32_t ncols, uint32_t n, bool flag, uint8_t *out, uint32_t &ol)
 {
     const uint32_t lane = threadIdx.x, nw = z.d.nw;
     const uint8_t *cons = P<uint8_t>(z, z.L.cons);
     if (flag) {
         const uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
-        const uint64_t *mem = P<uint64_t>(z, z.L.mem[z.cur]);
+        const uint64_t *mem = G_mem(z, z.cur);
         const uint32_t rend = i < ncols ? colrow[i] : z.R;
         for (uint32_t r0 = 0; r0 < rend; r0 += 64) {
             const uint32_t r = r0 + lane;
@@ -828,11 +1105,11 @@ __device__ void emit(Z &z, uint32_t i, uint32_t ncols, uint32_t n, bool flag, ui
 }
 
 // tidy_msa_bspoa (main.c:572): column-major MSA with mrow = n + 4
-__device__ void write_msa(Z &z, uint32_t ncols, uint32_t n, uint8_t *msa)
+__device__ __forceinline__ void write_msa(Z &z, uint32_t ncols, uint32_t n, uint8_t *msa)
 {
     const uint32_t lane = threadIdx.x, nw = z.d.nw, mrow = n + 4;
-    const uint8_t *nb = P<uint8_t>(z, z.L.nb[z.cur]);
-    const uint64_t *mem = P<uint64_t>(z, z.L.mem[z.cur]);
+    const uint8_t *nb = G_nb(z, z.cur);
+    const uint64_t *mem = G_mem(z, z.cur);
     const uint32_t *colof = P<uint32_t>(z, z.L.colof);
     const uint8_t *cons = P<uint8_t>(z, z.L.cons);
     const uint64_t tot = (uint64_t)ncols * mrow;
@@ -859,12 +1136,16 @@ __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
     z.ws = a.ws + z.d.ws_off;
     z.seq = a.seq + z.d.seq_off;
     z.lds = smem;
-    z.meta = smem + kRing * 256;
-    z.rd = reinterpret_cast<uint32_t *>(smem + kRing * 260);
+    z.meta = smem + kLdsMeta;
+    z.rd = reinterpret_cast<uint32_t *>(smem + kLdsFixed);
     z.pos = z.rd + a.lds_read_words;
     z.rdcap = a.lds_read_words * 16;
     z.status = kOk;
     z.cells = 0;
+    z.slow = 0;
+#pragma unroll
+    for (int i = 0; i < kProfSlots; ++i) z.pf[i] = 0;
+    const unsigned long long t_start = stamp();
     const uint32_t n = z.d.n;
     const uint32_t *soff = a.soff + z.d.seg0, *slen = a.slen + z.d.seg0;
     uint32_t *rdoff = P<uint32_t>(z, z.L.rdoff), *rdlen = P<uint32_t>(z, z.L.rdlen);
@@ -911,17 +1192,26 @@ __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
                     i = ncols;
                     break;
                 }
+                const unsigned long long tb0 = stamp();
                 i = find_breakpoint(z, ncols, n, colrate);
+                z.pf[kPfShred] += stamp() - tb0;
                 if (i >= 1) break;
             }
             if (z.status) break;
+            const unsigned long long te0 = stamp();
             emit(z, i, ncols, n, flag, out, ol);
+            z.pf[kPfShred] += stamp() - te0;
         }
     }
     if (lane == 0) {
         a.out_len[zi] = ol;
         a.status[zi] = z.status;
         a.cells[zi] = z.cells;
+        if (a.prof) {
+            z.pf[kPfTotal] = stamp() - t_start;
+#pragma unroll
+            for (int i = 0; i < kProfSlots; ++i) a.prof[(size_t)zi * kProfSlots + i] = z.pf[i];
+        }
     }
 }
 

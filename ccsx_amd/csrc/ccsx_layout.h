@@ -21,6 +21,9 @@ constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
 constexpr int kRing = 16;      // DP rows kept in LDS per wave
 constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+// fixed LDS words per wave: DP ring + ring meta + flush staging (codes, meta,
+// slots); the packed read and the shredding cursors follow (ccsx_kernel.hip)
+constexpr int kLdsFixedWords = kRing * 256 + kRing * 4 + 16 * 16 + 16 * 2 + 16 * 64;
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
 enum Status : int32_t {
@@ -50,8 +53,8 @@ struct ZmwDesc {
 };
 
 struct ZLayout {
-    uint64_t nb[2], mem[2], poff[2], pred[2];
-    uint64_t roff, rmx, rag, tof, spf, sslot, trace, spill;
+    uint64_t nb0, mem0, poff0, pred0, nb1, mem1, poff1, pred1;
+    uint64_t rmeta, spf, sslot, codes, slots, spill;
     uint64_t ev, tgt, ipt, iinf, ifix, cnt, fixf, addp, cntn;
     uint64_t colof, cons, cmask, colrow, rdoff, rdlen, rfirst, rlast, rfc, rlc;
     uint64_t total;
@@ -62,25 +65,25 @@ CCSX_HD inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255)
 CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 {
     uint64_t o = 0;
-    auto take = [&](uint64_t bytes) {
+    auto take = [&o](uint64_t bytes) {
         uint64_t r = o;
         o = align256(o + bytes);
         return r;
     };
-    for (int b = 0; b < 2; ++b) {
-        L.nb[b] = take(d.rcap);
-        L.mem[b] = take(uint64_t(d.rcap) * d.nw * 8);
-        L.poff[b] = take(uint64_t(d.rcap + 1) * 4);
-        L.pred[b] = take(uint64_t(d.ecap) * 4);
-    }
-    L.roff = take(uint64_t(d.rcap) * 4);
-    L.rmx = take(uint64_t(d.rcap) * 4);
-    L.rag = take(uint64_t(d.rcap) * 4);
-    L.tof = take(uint64_t(d.rcap) * 4);
-    L.spf = take(d.rcap);
-    L.sslot = take(uint64_t(d.rcap) * 4);
-    L.trace = take(uint64_t(d.rcap) * 64 + uint64_t(d.mcap) * 256);
-    L.spill = take(uint64_t(d.scap) * kW * 8);
+    L.nb0 = take(d.rcap);
+    L.mem0 = take(uint64_t(d.rcap) * d.nw * 8);
+    L.poff0 = take(uint64_t(d.rcap + 1) * 4);
+    L.pred0 = take(uint64_t(d.ecap) * 4);
+    L.nb1 = take(d.rcap);
+    L.mem1 = take(uint64_t(d.rcap) * d.nw * 8);
+    L.poff1 = take(uint64_t(d.rcap + 1) * 4);
+    L.pred1 = take(uint64_t(d.ecap) * 4);
+    L.rmeta = take(uint64_t(d.rcap) * 8);              // per DP row: band offset, multi-slot ordinal
+    L.spf = take(d.rcap);                              // per row: needed beyond the LDS ring
+    L.sslot = take(uint64_t(d.rcap) * 4);              // per spilled row: its spill record
+    L.codes = take(uint64_t(d.rcap) * 64);             // traceback codes, 4 bits/cell, 64 B/row
+    L.slots = take(uint64_t(d.mcap) * 256);            // predecessor slots of multi-predecessor rows
+    L.spill = take(uint64_t(d.scap) * (kW * 8 + 16));  // spilled rows: H/D + off/rmax/rarg
     L.ev = take(uint64_t(d.lcap) * 4);
     L.tgt = take(uint64_t(d.lcap) * 4);
     L.ipt = take(uint64_t(d.lcap) * 4);
@@ -135,6 +138,11 @@ struct KArgs {
     uint32_t nzmw;
     uint32_t lds_read_words;
     uint32_t lds_nmax;
+    unsigned long long *prof;  // optional: kProfSlots shader-clock counters per ZMW (diagnostics)
 };
+
+// phase counters written when KArgs::prof != nullptr
+enum ProfSlot { kPfTotal = 0, kPfLoad, kPfDp, kPfTrace, kPfMerge, kPfColumns, kPfShred, kPfRows,
+                kPfRowA, kPfRowB, kPfRowC, kPfRowD, kPfRowE, kPfFlush, kPfSpare0, kPfSpare1, kProfSlots };
 
 }  // namespace ccsx

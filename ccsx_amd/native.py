@@ -14,7 +14,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libccsx_amd.so")
+LIB_PATH = os.path.join(_HERE, os.environ.get("CCSX_LIB", "libccsx_amd.so"))
 
 MODE_SHRED = 0
 MODE_PRIMITIVE = 1
@@ -22,7 +22,8 @@ MODE_PRIMITIVE = 1
 # every symbol the public headers declare (checked by tests/test_abi.py)
 EXPORTS = {
     "ccsx_gpu.h": ["ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
-                   "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes"],
+                   "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
+                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw"],
     "ccsx_seqio.h": ["ccsx_reader_open", "ccsx_reader_next", "ccsx_reader_close"],
@@ -63,6 +64,8 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_fetch.argtypes = [C.c_void_p, C.POINTER(ZmwOut)]
         L.ccsx_gpu_staged_bytes.argtypes = [C.c_void_p]
         L.ccsx_gpu_staged_bytes.restype = C.c_uint64
+        L.ccsx_gpu_set_profiling.argtypes = [C.c_void_p, C.c_int]
+        L.ccsx_gpu_profile.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]
         L.ccsx_revcomp.argtypes = [C.c_char_p, C.c_uint32]
         L.ccsx_prepare.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]
@@ -248,6 +251,19 @@ class Engine:
         self.stage(zmws)
         self.launch(mode)
         return self.fetch()
+
+    PROF_SLOTS = ("total", "load_read", "dp", "traceback", "merge", "columns", "shred", "dp_rows",
+                  "row_A_place", "row_B_preds", "row_C_cells", "row_D_rowmax", "row_E_store", "flush", "spare0", "spare1")
+
+    def set_profiling(self, on: bool = True) -> None:
+        self._L.ccsx_gpu_set_profiling(self._ctx, 1 if on else 0)
+
+    def profile(self) -> dict:
+        """Per-phase shader-clock cycles summed over the last launch's ZMWs."""
+        buf = (C.c_uint64 * len(self.PROF_SLOTS))()
+        if self._L.ccsx_gpu_profile(self._ctx, buf, len(self.PROF_SLOTS)) != 0:
+            self._err("ccsx_gpu_profile")
+        return {k: int(buf[i]) for i, k in enumerate(self.PROF_SLOTS)}
 
     def staged_bytes(self) -> int:
         return int(self._L.ccsx_gpu_staged_bytes(self._ctx))

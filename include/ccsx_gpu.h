@@ -68,6 +68,12 @@ int ccsx_gpu_fetch(ccsx_ctx *ctx, ccsx_zmw_out *out);
 /* Device bytes the staged batch occupies (workspace + arenas). */
 uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *ctx);
 
+/* Diagnostics: per-phase shader-clock counters (s_memtime) summed over the
+ * ZMWs of the last launch: total, read staging, DP, traceback, merge,
+ * columns, breakpoint+emission, DP rows.  Off by default. */
+int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
+int ccsx_gpu_profile(ccsx_ctx *ctx, uint64_t *sums, uint32_t nslots);
+
 #ifdef __cplusplus
 }
 #endif

@@ -698,3 +698,38 @@ void ocsx_batch(int mode, int nthreads, uint32_t nz, const char **seqs, const ui
     free(tid);
     pthread_mutex_destroy(&b.mu);
 }
+
+/* Debug statistics of the current graph: hist[0] = rows, [1] = rows with >1
+ * predecessor, [2] = max in-degree, [3..] = rows having a predecessor further
+ * than 8, 16, 32, 64, 128 rows back. */
+void opoa_graph_stats(const opoa_t *g, uint64_t *hist)
+{
+    const graph_t *G = &g->g;
+    memset(hist, 0, 8 * sizeof(uint64_t));
+    hist[0] = G->R;
+    for (uint32_t r = 0; r < G->R; ++r) {
+        uint32_t np = G->poff[r + 1] - G->poff[r], far = 0;
+        if (np > 1) hist[1]++;
+        if (np > hist[2]) hist[2] = np;
+        for (uint32_t e = G->poff[r]; e < G->poff[r + 1]; ++e)
+            if (r - G->pred[e] > far) far = r - G->pred[e];
+        const uint32_t th[5] = {8, 16, 32, 64, 128};
+        for (int i = 0; i < 5; ++i)
+            if (far > th[i]) hist[3 + i]++;
+    }
+}
+
+/* Debug: rows of the current graph that have a successor further than `ring`
+ * rows ahead (the rows a kernel with a `ring`-row LDS ring must spill). */
+uint32_t opoa_spill_rows(const opoa_t *g, uint32_t ring)
+{
+    const graph_t *G = &g->g;
+    uint8_t *f = calloc(G->R + 1, 1);
+    for (uint32_t r = 0; r < G->R; ++r)
+        for (uint32_t e = G->poff[r]; e < G->poff[r + 1]; ++e)
+            if (r - G->pred[e] > ring) f[G->pred[e]] = 1;
+    uint32_t n = 0;
+    for (uint32_t r = 0; r < G->R; ++r) n += f[r];
+    free(f);
+    return n;
+}

@@ -1,0 +1,25 @@
+"""Per-phase cycle breakdown of the consensus kernel (s_memtime counters)."""
+import argparse, os, sys, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import ccsx_amd as cx
+ap = argparse.ArgumentParser()
+ap.add_argument("--L", type=int, default=10000)
+ap.add_argument("--passes", type=int, default=8)
+ap.add_argument("--n", type=int, default=1000)
+ap.add_argument("--mode", type=int, default=0)
+a = ap.parse_args()
+zs = [cx.prepare(cx.synth_zmw(20201104, h, a.L, a.passes)[0]) for h in range(a.n)]
+e = cx.Engine(0)
+e.stage(zs)
+e.launch(a.mode)
+e.set_profiling(True)
+ms = e.launch(a.mode)
+p = e.profile()
+res = e.fetch()
+cells = sum(r[2] for r in res)
+tot = p["total"]
+out = {"config": vars(a), "kernel_ms": ms, "gcups": cells / ms / 1e6,
+       "share": {k: round(v / tot, 4) for k, v in p.items() if k not in ("total", "dp_rows")},
+       "cycles_per_zmw": tot / a.n, "row_cycles": {k: round(v / max(p["dp_rows"], 1), 1) for k, v in p.items() if k.startswith("row_")}, "dp_cycles_per_row": p["dp"] / max(p["dp_rows"], 1),
+       "rows_per_zmw": p["dp_rows"] / a.n}
+print(json.dumps(out))
