@@ -89,6 +89,13 @@ static int fail(ccsx_ctx *c, const char *what, hipError_t e)
 
 extern "C" {
 
+int ccsx_gpu_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
 int ccsx_gpu_open(int device, ccsx_ctx **out)
 {
     *out = nullptr;

@@ -575,6 +575,31 @@ __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uin
 // ----------------------------------------------------------------------------
 constexpr uint32_t kTbRows = 32;
 
+// Traceback step tables indexed by (state << 4 | cell code), state 0 = H,
+// 1 = D, 2 = I; code = hcode | D-ext << 2 | iext << 3 (SPEC.md §3.4, §4).
+// kTbAct[state]: 4 bits per code {emit, move to predecessor, j -= 1, stop
+// (MSRC)}; kTbNext[state]: next state (4-bit fields).
+constexpr uint32_t tb_act(uint32_t st, uint32_t c)
+{
+    return st == 0 ? ((c & 3u) == 0 ? 0x7u : (c & 3u) == 1 ? 0x9u : 0u)  // MPRED: emit+pred+dj, MSRC: emit+stop
+         : st == 1 ? 0x2u                                               // D: move to the D slot's predecessor
+                   : 0x5u;                                              // I: emit INS, j -= 1
+}
+constexpr uint32_t tb_next(uint32_t st, uint32_t c)
+{
+    return st == 0 ? ((c & 3u) == 2 ? 1u : (c & 3u) == 3 ? 2u : 0u)
+         : st == 1 ? ((c >> 2) & 1u)
+                   : (((c >> 3) & 1u) ? 2u : 0u);
+}
+constexpr uint64_t tb_table(uint32_t st, bool act)
+{
+    uint64_t v = 0;
+    for (uint32_t c = 0; c < 16; ++c) v |= (uint64_t)(act ? tb_act(st, c) : tb_next(st, c)) << (c * 4);
+    return v;
+}
+constexpr uint64_t kTbAct[3] = {tb_table(0, true), tb_table(1, true), tb_table(2, true)};
+constexpr uint64_t kTbNext[3] = {tb_table(0, false), tb_table(1, false), tb_table(2, false)};
+
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
     const uint32_t lane = threadIdx.x;
@@ -585,9 +610,9 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     const uint2 *rmeta = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta);
     const uint8_t *codes = z.ws + z.L.codes;
     const uint8_t *slots = z.ws + z.L.slots;
-    int32_t *tbm = z.lds;                                                 // [kTbRows][4]: roff, mi-rel, p0, p1
-    uint32_t *tbpo = reinterpret_cast<uint32_t *>(z.lds + 4 * kTbRows);   // [kTbRows]: poff
-    uint32_t *tbnp = reinterpret_cast<uint32_t *>(z.lds + 5 * kTbRows);   // [kTbRows]: #predecessors
+    // LDS: per block row two 16-B records {roff, slot-row or kNone, np, poff}
+    // and {p0, p1, p2, p3}; then codes, slots and the staged events
+    uint4 *tbr = reinterpret_cast<uint4 *>(z.lds);  // [kTbRows][2]
     uint8_t *tbc = reinterpret_cast<uint8_t *>(z.lds + 256);              // kTbRows x 64 B codes
     uint8_t *tbs = reinterpret_cast<uint8_t *>(z.lds + 256 + 16 * kTbRows);  // slots of the block's multi rows
     uint32_t *evs = reinterpret_cast<uint32_t *>(z.lds + 256 + 16 * kTbRows + 64 * kTbRows);  // walk output
@@ -595,118 +620,109 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     static_assert(256 + 16 * kTbRows + 64 * kTbRows + kEvStage <= (uint32_t)kLdsFixedWords, "traceback LDS");
     uint32_t r = er, lead_row = 0, lead_j = 0;
     int32_t j = (int32_t)ej, st = 0, err = 0, done = 0;
-    uint64_t guard = 0;
-    const uint64_t glim = (uint64_t)z.R * 2 + (uint64_t)m * 2 + 16;
+    uint32_t guard = 0;
+    const uint32_t glim = z.R * 2u + m * 2u + 16u;
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
     while (!done) {
         const uint32_t blo = r >= kTbRows - 1 ? r - (kTbRows - 1) : 0u;
         const uint32_t nr = r - blo + 1;
-        uint32_t mi = kNone;
+        uint32_t mi = kNone, po = 0, np = 0, roff = 0;
         if (lane < nr) {
             const uint32_t row = blo + lane;
-            const uint32_t po = poff[row];
-            const uint32_t np = poff[row + 1] - po;
+            po = poff[row];
+            np = poff[row + 1] - po;
             const uint2 mt = rmeta[row];
+            roff = mt.x;
             mi = mt.y;
-            tbm[lane * 4 + 0] = (int32_t)mt.x;
-            tbm[lane * 4 + 2] = np > 0 ? (int32_t)pred[po] : 0;
-            tbm[lane * 4 + 3] = np > 1 ? (int32_t)pred[po + 1] : 0;
-            tbpo[lane] = po;
-            tbnp[lane] = np;
         }
+        const uint32_t p0 = lane < nr && np > 0 ? pred[po] : 0u;
+        const uint32_t p1 = lane < nr && np > 1 ? pred[po + 1] : 0u;
+        const uint32_t p2 = lane < nr && np > 2 ? pred[po + 2] : 0u;
+        const uint32_t p3 = lane < nr && np > 3 ? pred[po + 3] : 0u;
         // multi ordinals are increasing in row order: the block's slots are contiguous
         const uint32_t mi_lo = (uint32_t)wave_min((int32_t)(mi == kNone ? 0x7FFFFFFFu : mi));
         const uint32_t mi_hi = (uint32_t)wave_max((int32_t)(mi == kNone ? 0u : mi + 1));
         const uint32_t nms = mi_lo == 0x7FFFFFFFu ? 0u : mi_hi - mi_lo;
-        if (lane < nr) tbm[lane * 4 + 1] = (int32_t)(mi == kNone ? kNone : mi - mi_lo);
+        if (lane < nr) {
+            tbr[lane * 2] = make_uint4(roff, mi == kNone ? kNone : mi - mi_lo, np, po);
+            tbr[lane * 2 + 1] = make_uint4(p0, p1, p2, p3);
+        }
         for (uint32_t o = lane * 16; o < nr * 64; o += 1024)
             *reinterpret_cast<uint4 *>(tbc + o) = *reinterpret_cast<const uint4 *>(codes + (size_t)blo * 64 + o);
         for (uint32_t o = lane * 16; o < nms * 256; o += 1024)
             *reinterpret_cast<uint4 *>(tbs + o) = *reinterpret_cast<const uint4 *>(slots + (size_t)mi_lo * 256 + o);
         __syncthreads();
-        // The wave walks (uniform state).  Runs of diagonal steps -- MPRED on
-        // single-predecessor rows whose predecessor is the previous row, the
-        // bulk of any path -- are taken up to 64 at a time: lane i checks step
-        // i and a ballot finds the first break.  Other steps go one by one.
-        // Events go to LDS (a global store per step would stall the next step
-        // on its store-data wait) and are flushed by the wave.
+        DP_STAMP(kPfSpare0);
+        // lane 0 walks the block: per step one 16-B record read, one code
+        // byte, and for a multi-predecessor row one slot byte, all from LDS.
+        // Events are staged in LDS (a global store per step would stall the
+        // next step on its store-data wait) and flushed by the wave.
         const int32_t jhi = j;
-        uint32_t nev = 0;
-        while (r >= blo && nev + 64 <= kEvStage) {
-            if (++guard > glim) {
-                err = kErrTrace;
-                done = 1;
-                break;
-            }
-            if (st == 0) {
-                const int32_t rr = (int32_t)r - (int32_t)lane, jj = j - (int32_t)lane;
-                bool ok = rr >= (int32_t)blo && jj >= 1;
-                if (ok) {
-                    const uint32_t ri = (uint32_t)rr - blo;
-                    const int32_t *mt = tbm + ri * 4;
-                    const int32_t t = jj - mt[0];
-                    ok = t >= 0 && t < kW && tbnp[ri] == 1u && mt[2] == rr - 1;
-                    if (ok) ok = ((tbc[ri * 64 + (t >> 1)] >> ((t & 1) * 4)) & 3) == HC_MPRED;
-                }
-                const uint64_t bad = ~ballot(ok);
-                const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
-                if (k) {
-                    if (lane < k) evs[nev + lane] = (EV_ALN << 30) | (uint32_t)rr;
-                    nev += k;
-                    r -= k;
-                    j -= (int32_t)k;
-                    continue;
-                }
-            }
-            const uint32_t ri = r - blo;
-            const int32_t roff = uni(tbm[ri * 4]);
-            const uint32_t mrel = (uint32_t)uni(tbm[ri * 4 + 1]);
-            const uint32_t rp0 = (uint32_t)uni(tbm[ri * 4 + 2]), rp1 = (uint32_t)uni(tbm[ri * 4 + 3]);
-            const uint32_t t = (uint32_t)(j - roff);
-            const uint32_t c = (uint32_t)uni((int)((tbc[ri * 64 + (t >> 1)] >> ((t & 1u) * 4u)) & 15u));
-            auto pred_of = [&](uint32_t s) -> uint32_t {
-                return s == 0 ? rp0 : s == 1 ? rp1 : uni(pred[uni(tbpo[ri]) + s]);
-            };
-            if (st == 0) {
-                const uint32_t hc = c & 3u;
-                if (hc == HC_MPRED) {
-                    if (lane == 0) evs[nev] = (EV_ALN << 30) | r;
-                    ++nev;
-                    const uint32_t s = mrel != kNone ? (uint32_t)uni((int)tbs[mrel * 256 + (t >> 1) * 4 + (t & 1u)]) : 0u;
-                    r = pred_of(s);
-                    --j;
-                } else if (hc == HC_MSRC) {
-                    if (lane == 0) evs[nev] = (EV_ALN << 30) | r;
-                    ++nev;
-                    lead_row = r;
-                    lead_j = (uint32_t)j;
+        uint32_t nev = 0, far_pred = kNone;
+        if (lane == 0) {
+            // branch-free step: a 6-bit index (state, 4-bit cell code) selects
+            // the step's action from kTbAct (see SPEC.md §4)
+            uint32_t rr = r, stt = (uint32_t)st, ne = 0, g = guard, fp = kNone;
+            int32_t jj = j;
+            while (rr >= blo && ne < kEvStage) {
+                if (++g > glim) {
+                    err = kErrTrace;
                     done = 1;
                     break;
-                } else if (hc == HC_DEL) {
-                    st = 1;
-                } else {
-                    st = 2;
                 }
-            } else if (st == 1) {
-                const uint32_t s = mrel != kNone ? (uint32_t)uni((int)tbs[mrel * 256 + (t >> 1) * 4 + 2 + (t & 1u)]) : 0u;
-                st = (c >> 2) & 1u ? 1 : 0;
-                r = pred_of(s);
-            } else {
-                if (lane == 0) evs[nev] = (EV_INS << 30) | r;
-                ++nev;
-                st = (c >> 3) & 1u ? 2 : 0;
-                --j;
+                const uint32_t ri = rr - blo;
+                const uint4 rec = tbr[ri * 2];
+                const uint32_t t = (uint32_t)jj - rec.x;
+                const uint32_t c = (tbc[ri * 64 + (t >> 1)] >> ((t & 1u) << 2)) & 15u;
+                const uint64_t ta = stt == 0 ? kTbAct[0] : stt == 1 ? kTbAct[1] : kTbAct[2];
+                const uint64_t tn = stt == 0 ? kTbNext[0] : stt == 1 ? kTbNext[1] : kTbNext[2];
+                const uint32_t act = (uint32_t)(ta >> (c * 4)) & 15u;  // emit | pred | dj | stop
+                const uint32_t nst = (uint32_t)(tn >> (c * 4)) & 3u;
+                if (act & 1u) evs[ne++] = ((stt == 2 ? EV_INS : EV_ALN) << 30) | rr;
+                if (act & 8u) {
+                    lead_row = rr;
+                    lead_j = (uint32_t)jj;
+                    done = 1;
+                    break;
+                }
+                jj -= (int32_t)((act >> 2) & 1u);
+                if (act & 2u) {
+                    const uint32_t s = rec.y != kNone ? tbs[rec.y * 256 + (t >> 1) * 4 + (stt == 1 ? 2u : 0u) + (t & 1u)] : 0u;
+                    if (s >= 4) {
+                        fp = rec.w + s;
+                        stt = nst;
+                        break;
+                    }
+                    const uint4 pp = tbr[ri * 2 + 1];
+                    rr = s == 0 ? pp.x : s == 1 ? pp.y : s == 2 ? pp.z : pp.w;
+                }
+                stt = nst;
             }
+            r = rr, j = jj, st = (int32_t)stt, nev = ne, guard = g, far_pred = fp;
         }
+        DP_STAMP(kPfSpare1);
+        r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
+        j = __builtin_amdgcn_readfirstlane(j);
+        st = __builtin_amdgcn_readfirstlane(st);
+        done = __builtin_amdgcn_readfirstlane(done);
+        err = __builtin_amdgcn_readfirstlane(err);
+        guard = (uint32_t)__builtin_amdgcn_readfirstlane((int)guard);
         nev = (uint32_t)__builtin_amdgcn_readfirstlane((int)nev);
+        lead_row = (uint32_t)__builtin_amdgcn_readfirstlane((int)lead_row);
+        lead_j = (uint32_t)__builtin_amdgcn_readfirstlane((int)lead_j);
+        far_pred = (uint32_t)__builtin_amdgcn_readfirstlane((int)far_pred);
+        if (far_pred != kNone) r = uni(pred[far_pred]);  // the step's predecessor, slot >= 4
+        __syncthreads();
         for (uint32_t i = lane; i < nev; i += 64) ev[jhi - (int32_t)i] = evs[i];
         __syncthreads();
+        DP_STAMP(kPfFlush);
     }
     if (err) {
         z.status = err;
         return;
     }
-    lead_row = uni(lead_row);
-    lead_j = uni(lead_j);
     for (uint32_t jj = lane; jj < lead_j; jj += 64) ev[jj] = (EV_LEAD << 30) | lead_row;
     __syncthreads();
 }

@@ -21,7 +21,7 @@ MODE_PRIMITIVE = 1
 
 # every symbol the public headers declare (checked by tests/test_abi.py)
 EXPORTS = {
-    "ccsx_gpu.h": ["ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
+    "ccsx_gpu.h": ["ccsx_gpu_device_count", "ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
                    "ccsx_gpu_set_profiling", "ccsx_gpu_profile"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],

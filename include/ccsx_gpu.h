@@ -49,6 +49,9 @@ typedef struct {
     uint64_t cells;           /* DP cells computed for this ZMW */
 } ccsx_zmw_out;
 
+/* Number of HIP devices visible to this process (0 if none). */
+int ccsx_gpu_device_count(void);
+
 /* Open a context on HIP device `device`. */
 int ccsx_gpu_open(int device, ccsx_ctx **ctx);
 void ccsx_gpu_close(ccsx_ctx *ctx);

@@ -1,0 +1,45 @@
+"""End to end: the C host program (ccsx_amd/bin/ccsx) on a synthetic subread
+FASTA vs the oracle applied to the same records (ingest, filters, prepare,
+shredded / -P consensus, ordered FASTA output)."""
+import os
+import subprocess
+
+import pytest
+
+import ccsx_amd as cx
+from oracle.oracle import Poa
+from tools.gen_synth import write
+
+pytestmark = pytest.mark.gpu
+BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ccsx_amd", "bin", "ccsx")
+
+
+def _expected(path, mode, min_count=3, mn=5000, mx=500000, exclude=()):
+    out = []
+    g = Poa()
+    for movie, hole, subs in cx.read_zmws(path):
+        if len(subs) < min_count + 2 or not (mn <= sum(map(len, subs)) <= mx) or hole in exclude:
+            continue
+        p = cx.prepare(subs)
+        ccs = g.zmw(p.seqs, p.offs, p.lens, mode)
+        if ccs:
+            out.append(b">%s/%s/ccs\n%s\n" % (movie.encode(), hole.encode(), ccs))
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("mode_flag,mode", [([], 0), (["-P"], 1)])
+def test_cli_matches_oracle(tmp_path, mode_flag, mode):
+    fa = str(tmp_path / "in.fa")
+    write(fa, 12, 1500, 7)
+    # a ZMW with too few subreads and one outside -m are filtered out
+    with open(fa, "ab") as f:
+        f.write(b">synth/900/0_10\nACGTACGTAC\n")
+        subs, _ = cx.synth_zmw(20201104, 901, 300, 8)
+        for i, s in enumerate(subs):
+            f.write(b">synth/901/%d_%d\n%s\n" % (i, i + 1, s))
+    out = str(tmp_path / "out.fa")
+    r = subprocess.run([BIN, "-A", "-j", "2", "-X", "3,5"] + mode_flag + [fa, out], capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    got = open(out, "rb").read()
+    assert got == _expected(fa, mode, exclude={"3", "5"})
+    assert got.count(b">") == 10

@@ -20,6 +20,6 @@ cells = sum(r[2] for r in res)
 tot = p["total"]
 out = {"config": vars(a), "kernel_ms": ms, "gcups": cells / ms / 1e6,
        "share": {k: round(v / tot, 4) for k, v in p.items() if k not in ("total", "dp_rows")},
-       "cycles_per_zmw": tot / a.n, "row_cycles": {k: round(v / max(p["dp_rows"], 1), 1) for k, v in p.items() if k.startswith("row_")}, "dp_cycles_per_row": p["dp"] / max(p["dp_rows"], 1),
+       "cycles_per_zmw": tot / a.n, "row_cycles": {k: round(v / max(p["dp_rows"], 1), 1) for k, v in p.items() if k.startswith("row_")}, "tb_share": {k: round(p[k] / tot, 4) for k in ("spare0", "spare1", "flush")}, "dp_cycles_per_row": p["dp"] / max(p["dp_rows"], 1),
        "rows_per_zmw": p["dp_rows"] / a.n}
 print(json.dumps(out))
