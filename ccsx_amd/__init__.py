@@ -5,6 +5,6 @@ gfx950 + C-ABI, include/*.h); this package holds its build script and ctypes
 bindings.
 """
 from .native import (MODE_PRIMITIVE, MODE_SHRED, Engine, GpuError, Prepared, lib, pairwise, prepare,  # noqa: F401
-                     prepare_segments, read_zmws, revcomp, synth_zmw)
+                     prepare_segments, read_calls, read_zmws, revcomp, synth_zmw)
 
 __version__ = "0.1.0"

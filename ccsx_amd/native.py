@@ -154,8 +154,11 @@ def pairwise(q: bytes, t: bytes) -> dict:
     return {n if n != "del_" else "del": getattr(r, n) for n, _ in PairAln._fields_}
 
 
-def read_zmws(path: str, is_bam: bool = False):
-    """Yield (movie, hole, [subreads]) per kseq_zmw_read (seqio.h:152-201); stops at the first -1."""
+def read_calls(path: str, is_bam: bool = False):
+    """Yield every ccsx_reader_next result the way main.c step 0 drives
+    kseq_zmw_read (main.c:658-697): (n, movie, hole, [subreads]) for a ZMW,
+    (-1, None, None, None) for each -1; after a -1 the next chunk reads on,
+    and the input ends at the first chunk that yields no ZMW."""
     L = lib()
     r = L.ccsx_reader_open(path.encode(), 1 if is_bam else 0)
     if not r:
@@ -165,18 +168,31 @@ def read_zmws(path: str, is_bam: bool = False):
         sq = C.c_void_p()
         ln = C.POINTER(C.c_uint32)()
         while True:
-            n = L.ccsx_reader_next(r, C.byref(mv), C.byref(hl), C.byref(sq), C.byref(ln))
-            if n < 0:
+            got = 0
+            while True:
+                n = L.ccsx_reader_next(r, C.byref(mv), C.byref(hl), C.byref(sq), C.byref(ln))
+                if n < 0:
+                    yield n, None, None, None
+                    break
+                got += 1
+                lens = [ln[i] for i in range(n)]
+                raw = C.string_at(sq, sum(lens))
+                subs, o = [], 0
+                for x in lens:
+                    subs.append(raw[o:o + x])
+                    o += x
+                yield n, mv.value.decode(), hl.value.decode(), subs
+            if not got:
                 break
-            lens = [ln[i] for i in range(n)]
-            raw = C.string_at(sq, sum(lens))
-            subs, o = [], 0
-            for x in lens:
-                subs.append(raw[o:o + x])
-                o += x
-            yield mv.value.decode(), hl.value.decode(), subs
     finally:
         L.ccsx_reader_close(r)
+
+
+def read_zmws(path: str, is_bam: bool = False):
+    """Yield (movie, hole, [subreads]) per ZMW, as the CLI's step 0 sees them."""
+    for n, movie, hole, subs in read_calls(path, is_bam):
+        if n >= 0:
+            yield movie, hole, subs
 
 
 # ---------------------------------------------------------------- GPU engine

@@ -104,11 +104,14 @@ def test_reader_fastq_gz_crlf(tmp_path):
 
 
 def test_reader_invalid_name_ends_call(tmp_path):
-    """seqio.h:168-172: an invalid name returns -1 (the caller stops)."""
+    """seqio.h:168-172: an invalid name returns -1; main.c's next chunk reads on
+    from the pending record (main.c:658-697)."""
     fa = ">m/1/0_2\nAC\n>m/2/0_2\nGG\n>bad_name\nTT\n>m/3/0_2\nCC\n"
     p = tmp_path / "b.fa"
     _write(p, fa)
-    assert list(cx.read_zmws(str(p))) == [("m", "1", [b"AC"])]
+    calls = [(n, h, s) for n, _, h, s in cx.read_calls(str(p))]
+    assert calls == [(1, "1", [b"AC"]), (-1, None, None), (1, "2", [b"GG"]), (1, "3", [b"CC"]), (-1, None, None),
+                     (-1, None, None)]
 
 
 def test_reader_bam(tmp_path):
