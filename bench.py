@@ -42,11 +42,27 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 OPS_PER_CELL = 10
 
 
+def rank_holes(cfg: dict, rank: int) -> range:
+    """Hole ids of one rank: contiguous, disjoint ranges (weak scaling)."""
+    return range(rank * cfg["nzmw"], (rank + 1) * cfg["nzmw"])
+
+
+def aggregate(dist, elapsed: float, cells_per_step: int):
+    """(max elapsed over ranks, total cells per step over ranks); dist may be None."""
+    if dist is None:
+        return elapsed, float(cells_per_step)
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([float(cells_per_step)], dtype=torch.float64)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(c.item())
+
+
 def make_batch(cfg: dict, rank: int):
     import ccsx_amd as cx
     zs = []
-    base = rank * cfg["nzmw"]
-    for h in range(base, base + cfg["nzmw"]):
+    for h in rank_holes(cfg, rank):
         subs, _ = cx.synth_zmw(SEED, h, cfg["L"], cfg["passes"])
         zs.append(cx.prepare(subs))
     return zs
@@ -125,16 +141,7 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([float(cells_per_step)], dtype=torch.float64)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        cells_total_step = float(c.item())
-    else:
-        cells_total_step = float(cells_per_step)
+    elapsed, cells_total_step = aggregate(dist, elapsed, cells_per_step)
 
     if rank == 0:
         n_total = cfg["nzmw"] * world * args.steps
