@@ -33,6 +33,9 @@ CONFIGS = {
               nzmw=1000, L=20000, passes=5, mode=1),
     "D": dict(workload="D: 10000 ZMWs x 2 kb insert x 30 passes, 10% error, shredded mode",
               nzmw=10000, L=2000, passes=30, mode=0),
+    # a per-GPU slice of config E (500k ZMWs, mixed 5-25 kb inserts, 5-12 passes)
+    "E": dict(workload="E-slice: 2000 ZMWs per GPU, insert ~U[5,25] kb x passes ~U[5,12] (total <= 450 kb), "
+                       "10% error, shredded mode", nzmw=2000, L=0, passes=0, mode=0),
 }
 SEED = 20201104
 # gfx950 integer VALU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 int32 lane-ops/s
@@ -59,11 +62,26 @@ def aggregate(dist, elapsed: float, cells_per_step: int):
     return float(t.item()), float(c.item())
 
 
+def zmw_shape(cfg: dict, hole: int):
+    """(insert length, passes) of one hole; config E draws them per hole."""
+    if cfg["L"]:
+        return cfg["L"], cfg["passes"]
+    x = (hole * 0x9E3779B97F4A7C15 + SEED) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 31
+    x = (x * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 29
+    L = 5000 + x % 20001
+    passes = 5 + (x >> 20) % 8
+    passes = max(5, min(passes, 450000 // (L * 11 // 10)))
+    return L, passes
+
+
 def make_batch(cfg: dict, rank: int):
     import ccsx_amd as cx
     zs = []
     for h in rank_holes(cfg, rank):
-        subs, _ = cx.synth_zmw(SEED, h, cfg["L"], cfg["passes"])
+        L, passes = zmw_shape(cfg, h)
+        subs, _ = cx.synth_zmw(SEED, h, L, passes)
         zs.append(cx.prepare(subs))
     return zs
 
@@ -163,8 +181,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (SURVEY.md §8d generator, seed 20201104, per-rank hole ranges)",
-            "config": {"workload": cfg["workload"], "zmws_per_gpu": cfg["nzmw"], "insert_len": cfg["L"],
-                       "passes": cfg["passes"], "mode": "shredded" if cfg["mode"] == 0 else "primitive",
+            "config": {"workload": cfg["workload"], "zmws_per_gpu": cfg["nzmw"], "insert_len": cfg["L"] or "5000-25000",
+                       "passes": cfg["passes"] or "5-12", "mode": "shredded" if cfg["mode"] == 0 else "primitive",
                        "parallelism": f"hole-batch sharding x{world}, no collectives"},
             "gcups": round(cells_total_step * args.steps / elapsed / 1e9, 3),
             "cells_per_step": int(cells_total_step),

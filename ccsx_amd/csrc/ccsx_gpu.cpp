@@ -64,7 +64,7 @@ struct ccsx_ctx {
     bool profiling = false;
     DevBuf d_prof;
     std::vector<unsigned long long> h_prof;
-    DevBuf d_seq, d_soff, d_slen, d_desc, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
+    DevBuf d_seq, d_soff, d_slen, d_desc, d_order, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
     // fetched results
     std::vector<uint8_t> h_out;
     std::vector<uint32_t> h_olen, h_ncols;
@@ -118,7 +118,7 @@ void ccsx_gpu_close(ccsx_ctx *c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    DevBuf *bufs[] = {&c->d_prof, &c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_ws, &c->d_out,
+    DevBuf *bufs[] = {&c->d_prof, &c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_order, &c->d_ws, &c->d_out,
                       &c->d_msa, &c->d_olen, &c->d_ncols, &c->d_status, &c->d_cells};
     for (DevBuf *b : bufs) b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -203,6 +203,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, c->d_soff.reserve(size_t(nseg) * 4));
     HIPCHK(c, c->d_slen.reserve(size_t(nseg) * 4));
     HIPCHK(c, c->d_desc.reserve(nz * sizeof(ccsx::ZmwDesc)));
+    HIPCHK(c, c->d_order.reserve(nz * 4));
     HIPCHK(c, c->d_ws.reserve(ws_b));
     HIPCHK(c, c->d_out.reserve(out_b));
     HIPCHK(c, c->d_msa.reserve(msa_b));
@@ -229,6 +230,14 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, hipMemcpyAsync(c->d_slen.p, hlen.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_desc.p, c->desc.data(), nz * sizeof(ccsx::ZmwDesc), hipMemcpyHostToDevice,
                              c->stream));
+    // launch order: decreasing total bases (the POA work of a ZMW grows with
+    // it in both modes), ties in input order
+    std::vector<uint32_t> order(nz);
+    for (size_t i = 0; i < nz; ++i) order[i] = uint32_t(i);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+        return c->desc[x].rcap > c->desc[y].rcap;
+    });
+    HIPCHK(c, hipMemcpyAsync(c->d_order.p, order.data(), nz * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -248,6 +257,7 @@ int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
     a.soff = c->d_soff.as<uint32_t>();
     a.slen = c->d_slen.as<uint32_t>();
     a.desc = c->d_desc.as<ccsx::ZmwDesc>();
+    a.order = c->d_order.as<uint32_t>();
     a.ws = c->d_ws.as<uint8_t>();
     a.out = c->d_out.as<uint8_t>();
     a.msa = c->d_msa.as<uint8_t>();

@@ -59,6 +59,33 @@ __device__ __forceinline__ int wave_incl_max(int v)
     return v;
 }
 
+// two independent inclusive max-scans, interleaved so each DPP op's hazard
+// wait is covered by the other chain's op (one s_nop 0 per pair instead of
+// two s_nop 1)
+__device__ __forceinline__ void wave_incl_max2(int &a, int &b)
+{
+    asm("s_nop 1\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_i32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_i32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_i32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_i32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "v_max_i32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "v_max_i32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(a), "+v"(b));
+}
+
 __device__ __forceinline__ int wave_incl_sum(int v)
 {
     v += dpp<0x111>(0, v);
@@ -197,7 +224,7 @@ struct PredRow {
 
 // LDS layout of one wave (int32 words)
 constexpr int kLdsRing = 0;                          // kRing rows x [Hev|Hod|Dev|Dod] x 64
-constexpr int kLdsMeta = kRing * 256;                // kRing x {off, rmax, rarg, -}
+constexpr int kLdsMeta = kRing * 256;                // (spare) kRing x 4 words
 constexpr int kLdsStCodes = kLdsMeta + kRing * 4;    // kBlk rows x 64 B of codes
 constexpr int kBlk = 16;                             // rows per flush block
 constexpr int kLdsStMeta = kLdsStCodes + kBlk * 16;  // kBlk x {off, mi}
@@ -206,13 +233,11 @@ constexpr int kLdsFixed = kLdsStSlots + kBlk * 64;   // then: packed read codes,
 static_assert(kBlk == kRing, "the ring doubles as the spill source of a flushed block");
 static_assert(kLdsFixed == kLdsFixedWords, "host and device LDS layouts disagree");
 
+// meta of a spilled row (rows within the ring keep theirs in registers, DpState)
 __device__ __forceinline__ PredRow pred_meta(const Z &z, uint32_t r, uint32_t p)
 {
     PredRow m;
-    if (r - p <= (uint32_t)kRing) {
-        const int32_t *mt = z.lds + kLdsMeta + (p % kRing) * 4;
-        m.off = mt[0], m.rmax = mt[1], m.rarg = mt[2];
-    } else {
+    {
         const uint32_t sl = uni(__builtin_nontemporal_load(P<uint32_t>(z, z.L.sslot) + p));
         const int32_t *rec = reinterpret_cast<const int32_t *>(z.ws + z.L.spill + (size_t)sl * (kW * 8 + 16));
         m.off = uni(__builtin_nontemporal_load(rec + 256));
@@ -241,17 +266,21 @@ __device__ __forceinline__ void pin(FlushBuf &f)
 // ----------------------------------------------------------------------------
 // SPEC.md §3: banded read-vs-graph DP for one read (codes in z.rd, length m)
 // ----------------------------------------------------------------------------
-// per lane: row r0+lane's base | spill flag << 2 | npred << 8, poff, first 4 predecessors
+// per lane: row r0+lane's info (base | spill << 2 | chain << 3 | npred << 8;
+// chain = the only predecessor is the previous row), poff, first 4 predecessors
 struct RowPre {
     uint32_t info, po, p0, p1, p2, p3;
 };
+constexpr uint32_t kInfoSpill = 4u, kInfoChain = 8u;
 
 struct DpState {
     int32_t bE;
-    uint32_t bR, bJ;
+    uint32_t bKey;                   // best end cell: row * 2 + (0: t0, 1: t1) of this lane
     uint32_t nmulti, nspill;
-    int32_t pH0, pH1, pD0, pD1, pOff, pRm, pRarg;  // row r-1 (registers)
-    RowPre cur, nxt;  // rows of the current / next 64-row superblock (one row per lane)
+    int32_t pH0, pH1, pD0, pD1;      // row r-1, this lane's two cells (registers)
+    int32_t pOff, pRm, pRarg;        // row r-1 meta (uniform)
+    int32_t mOff, mRm, mRarg;        // meta ring: lane (r % kRing) holds row r's meta
+    RowPre cur, nxt;                 // rows of the current / next 64-row superblock (one row per lane)
 };
 
 __device__ __forceinline__ void prefetch_rows(const Z &z, uint32_t r0, RowPre &o)
@@ -267,8 +296,94 @@ __device__ __forceinline__ void prefetch_rows(const Z &z, uint32_t r0, RowPre &o
         o.p1 = np > 1 ? pred[o.po + 1] : 0u;
         o.p2 = np > 2 ? pred[o.po + 2] : 0u;
         o.p3 = np > 3 ? pred[o.po + 3] : 0u;
-        o.info = ((uint32_t)nb[rr] & 3u) | ((uint32_t)P<uint8_t>(z, z.L.spf)[rr] << 2) | (np << 8);
+        const uint32_t chain = (np == 1 && o.p0 + 1 == rr) ? kInfoChain : 0u;
+        o.info = ((uint32_t)nb[rr] & 3u) | ((uint32_t)P<uint8_t>(z, z.L.spf)[rr] << 2) | chain | (np << 8);
     }
+}
+
+// The cells of one row given the predecessor terms (SPEC.md §3.2-§3.5).
+// hA = max_s Hp_s(j0-1) (= Mh of t0), hB = Mh of t1, Dv0/Dv1 and their slot /
+// ext bits computed by the caller.  FULL: every cell of the band is valid.
+struct RowOut {
+    int32_t H0, H1, D0, D1, rm, rarg;
+    uint32_t code;  // two 4-bit cell codes (t0 low nibble)
+};
+
+template <bool FULL>
+__device__ __forceinline__ RowOut row_cells(const Z &z, DpState &S, uint32_t r, int32_t off, uint32_t m, uint32_t base,
+                                            int32_t Mh0, int32_t Mh1, int32_t Dv0, int32_t Dv1, uint32_t dx0,
+                                            uint32_t dx1)
+{
+    const int lane = threadIdx.x;
+    const int32_t t0 = 2 * lane;
+    const int32_t j0 = off + t0, j1 = j0 + 1;
+    // read codes of the two cells: one ds_read2 of the packed read
+    const uint32_t w = (uint32_t)j0 >> 4;
+    const uint64_t wd = (uint64_t)z.rd[w] | ((uint64_t)z.rd[w + 1] << 32);
+    const uint32_t sh = ((uint32_t)j0 & 15u) * 2u;
+    const uint32_t q0 = (uint32_t)(wd >> sh) & 3u, q1 = (uint32_t)(wd >> (sh + 2)) & 3u;
+    // M (SPEC.md §3.2)
+    int32_t src0 = kO + kE * j0;
+    if (off == 0) src0 = lane == 0 ? 0 : src0;
+    const int32_t src1 = kO + kE * j1;
+    const bool mp0 = Mh0 >= src0, mp1 = Mh1 >= src1;
+    const int32_t M0 = (mp0 ? Mh0 : src0) + (base == q0 ? kMs : kXs);
+    const int32_t M1 = (mp1 ? Mh1 : src1) + (base == q1 ? kMs : kXs);
+    uint32_t hc0 = mp0 ? HC_MPRED : HC_MSRC, hc1 = mp1 ? HC_MPRED : HC_MSRC;
+    const bool d0 = Dv0 > M0, d1 = Dv1 > M1;
+    const int32_t hp0 = d0 ? Dv0 : M0, hp1 = d1 ? Dv1 : M1;
+    hc0 = d0 ? HC_DEL : hc0;
+    hc1 = d1 ? HC_DEL : hc1;
+    // in-row insertions (SPEC.md §3.4): exclusive prefix max of X = H' - E*t.
+    // The row max of H equals the row max of H' (an insertion is always
+    // below the H' it extends from) and so does its first position, so the
+    // row-max reduction runs beside the scan instead of after it.
+    const int32_t X0 = hp0 - kE * t0, X1 = hp1 - kE * (t0 + 1);
+    int32_t hm0 = hp0, hm1 = hp1;
+    if (!FULL) {
+        if (j0 >= (int32_t)m) hm0 = kNeg;
+        if (j1 >= (int32_t)m) hm1 = kNeg;
+    }
+    int32_t incl = max(X0, X1), rmx = max(hm0, hm1);
+    wave_incl_max2(incl, rmx);
+    const int32_t Pex = wave_shr1(kNeg, incl);
+    const int32_t ex1 = max(Pex, X0);
+    const int32_t I0 = lane == 0 ? kNeg : kO + kE * t0 + Pex;
+    const int32_t I1 = kO + kE * (t0 + 1) + ex1;
+    const uint32_t iext1 = Pex > X0 ? 8u : 0u;
+    const uint32_t iext0 = (uint32_t)wave_shr1(0, ex1 > X1 ? 8 : 0);
+    const bool i0 = I0 > hp0, i1 = I1 > hp1;
+    RowOut o;
+    o.H0 = i0 ? I0 : hp0;
+    o.H1 = i1 ? I1 : hp1;
+    o.D0 = Dv0;
+    o.D1 = Dv1;
+    hc0 = i0 ? HC_INS : hc0;
+    hc1 = i1 ? HC_INS : hc1;
+    uint32_t c0 = hc0 | dx0 | iext0, c1 = hc1 | dx1 | iext1;
+    if (!FULL) {
+        if (j0 >= (int32_t)m) o.H0 = kNeg, o.D0 = kNeg, c0 = 0;
+        if (j1 >= (int32_t)m) o.H1 = kNeg, o.D1 = kNeg, c1 = 0;
+    }
+    o.code = c0 | (c1 << 4);
+    // row max / argmax for the successors' band placement
+    o.rm = __builtin_amdgcn_readlane(rmx, 63);
+    const uint64_t hit0 = ballot(hm0 == o.rm), hit1 = ballot(hm1 == o.rm);
+    const uint32_t c0i = hit0 ? 2u * (uint32_t)__builtin_ctzll(hit0) : 256u;
+    const uint32_t c1i = hit1 ? 2u * (uint32_t)__builtin_ctzll(hit1) + 1u : 256u;
+    o.rarg = off + (int32_t)(c0i < c1i ? c0i : c1i);
+    // free-end candidates (SPEC.md §3.5): e = H + 2j - 2m - 1, or H at j = m-1
+    const int32_t eb = 2 * j0 - 2 * (int32_t)m - 1;
+    int32_t e0 = o.H0 + eb, e1 = o.H1 + eb + 2;
+    if (j0 == (int32_t)m - 1) e0 = o.H0;
+    if (j1 == (int32_t)m - 1) e1 = o.H1;
+    if (!FULL) {
+        if (j0 >= (int32_t)m) e0 = INT32_MIN;
+        if (j1 >= (int32_t)m) e1 = INT32_MIN;
+    }
+    if (e0 > S.bE) S.bE = e0, S.bKey = r * 2;
+    if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1;
+    return o;
 }
 
 // one 16-row block of the DP, then its flush through register set f.
@@ -283,10 +398,9 @@ __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_
     if (r0 >= R) return;
     const uint32_t *pred = G_pred(z, z.cur);
     const int32_t lim = m > (uint32_t)kW ? (int32_t)(m - kW) : 0;
-    const int t0 = 2 * lane, t1 = 2 * lane + 1;
-    int32_t *st_meta = z.lds + kLdsStMeta;
     uint8_t *st_codes = reinterpret_cast<uint8_t *>(z.lds + kLdsStCodes);
     uint32_t *st_slots = reinterpret_cast<uint32_t *>(z.lds + kLdsStSlots);
+    int32_t *st_meta = z.lds + kLdsStMeta;
     const uint32_t mi0 = S.nmulti;
     if ((blk & 3u) == 0) {
         if (blk == 0) prefetch_rows(z, 0, S.cur);
@@ -304,56 +418,22 @@ __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_
         DP_STAMP(kPfRowE);
         const int li = (int)(r & 63u);
         const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.info, li);
-        const uint32_t base = info & 3u, sp = (info >> 2) & 1u, np = info >> 8;
-        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p0, li);
-        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p1, li);
-        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p2, li);
-        const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p3, li);
-        const uint32_t po = SLOW ? (uint32_t)__builtin_amdgcn_readlane((int)S.cur.po, li) : 0u;
+        const uint32_t base = info & 3u, np = info >> 8;
         if (np > 255u) {
             z.status = kErrInDegree;
             return;
         }
-        auto predp = [&](uint32_t s) -> uint32_t {
-            if (s == 0) return p0;
-            if (s == 1) return p1;
-            if (s == 2) return p2;
-            if (s == 3 || !SLOW) return p3;
-            return uni(pred[po + s]);
-        };
-        // band placement (SPEC.md §3.1).  Common case -- the only predecessor
-        // is row r-1 -- from registers; otherwise from the LDS ring meta
-        // (row r-1 included) or, in SLOW mode, a spilled row's record.
-        auto meta = [&](uint32_t p) -> PredRow {
-            if (!SLOW || r - p <= (uint32_t)kRing) {
-                const int32_t *mt = z.lds + kLdsMeta + (p % kRing) * 4;
-                return PredRow{mt[0], mt[1], mt[2]};
-            }
-            return pred_meta(z, r, p);
-        };
-        const bool chain = np == 1 && p0 + 1 == r;
-        int32_t off = 0;
-        if (chain) {
-            off = S.pRarg + 1 - kW / 2;
-        } else if (np) {
-            const PredRow m0 = meta(p0);
-            int32_t bm = m0.rmax, barg = m0.rarg;
-            for (uint32_t s = 1; s < np; ++s) {
-                const PredRow pm = meta(predp(s));
-                if (pm.rmax > bm) bm = pm.rmax, barg = pm.rarg;
-            }
-            off = barg + 1 - kW / 2;
-        }
-        off = off < 0 ? 0 : off;
-        off = off > lim ? lim : off;
-        DP_STAMP(kPfRowA);
-        // predecessor terms (SPEC.md §3.2)
-        int32_t Mh0 = kNeg, Mh1 = kNeg, Dv0 = kNeg, Dv1 = kNeg;
-        uint32_t ms0 = 0, ms1 = 0, ds0 = 0, ds1 = 0, dx0 = 0, dx1 = 0;
-        const int32_t sh1 = off - S.pOff;
-        if (chain && (uint32_t)sh1 <= 2u) {
-            // fast path: the only predecessor is the previous row, band shift
-            // 0..2 -> its cells come from registers through DPP lane shifts
+        RowOut o;
+        uint32_t mi = kNone;
+        int32_t off;
+        const int32_t chain_off = min(max(S.pRarg + 1 - kW / 2, 0), lim);
+        const int32_t sh1 = chain_off - S.pOff;
+        if ((info & kInfoChain) && (uint32_t)sh1 <= 2u && chain_off + kW <= (int32_t)m) {
+            // fast path: the only predecessor is the previous row, the band
+            // moved by 0..2 and is entirely inside the read: the predecessor's
+            // cells come from registers through DPP lane shifts
+            off = chain_off;
+            
             int hA, hB, hC, dB, dC;
             if (sh1 == 0) {
                 hA = wave_shr1(kNeg, S.pH1), hB = S.pH0, hC = S.pH1, dB = S.pD0, dC = S.pD1;
@@ -363,18 +443,54 @@ __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_
                 hA = S.pH1, hB = wave_shl1(kNeg, S.pH0), hC = wave_shl1(kNeg, S.pH1);
                 dB = wave_shl1(kNeg, S.pD0), dC = wave_shl1(kNeg, S.pD1);
             }
-            Mh0 = hA, Mh1 = hB;
-            {
-                const int a = hB + kO + kE, b = dB + kE;
-                const int c = b > a ? b : a;
-                if (c > kNeg) Dv0 = c, dx0 = b > a;
-            }
-            {
-                const int a = hC + kO + kE, b = dC + kE;
-                const int c = b > a ? b : a;
-                if (c > kNeg) Dv1 = c, dx1 = b > a;
-            }
+            // D = max(H+O+E, D+E) with NEG floor; ext only if it beats NEG
+            const int a0 = hB + kO + kE, b0 = dB + kE, a1 = hC + kO + kE, b1 = dC + kE;
+            const int32_t Dv0 = max(max(a0, b0), kNeg), Dv1 = max(max(a1, b1), kNeg);
+            const uint32_t dx0 = b0 > max(a0, kNeg) ? 4u : 0u, dx1 = b1 > max(a1, kNeg) ? 4u : 0u;
+            
+            o = row_cells<true>(z, S, r, off, m, base, hA, hB, Dv0, Dv1, dx0, dx1);
+            DP_STAMP(kPfRowA);  // fast (chain) rows
+#ifdef CCSX_DP_STAMPS
+            z.pf[kPfRowD] += 1;  // number of fast rows
+#endif
         } else {
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p0, li);
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p1, li);
+            const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p2, li);
+            const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p3, li);
+            const uint32_t po = SLOW ? (uint32_t)__builtin_amdgcn_readlane((int)S.cur.po, li) : 0u;
+            auto predp = [&](uint32_t s) -> uint32_t {
+                if (s == 0) return p0;
+                if (s == 1) return p1;
+                if (s == 2) return p2;
+                if (s == 3 || !SLOW) return p3;
+                return uni(pred[po + s]);
+            };
+            // meta of a predecessor: from the register meta ring (rows within
+            // kRing) or, in SLOW mode, a spilled row's record
+            auto meta = [&](uint32_t p) -> PredRow {
+                if (!SLOW || r - p <= (uint32_t)kRing) {
+                    const int l = (int)(p % kRing);
+                    return PredRow{__builtin_amdgcn_readlane(S.mOff, l), __builtin_amdgcn_readlane(S.mRm, l),
+                                   __builtin_amdgcn_readlane(S.mRarg, l)};
+                }
+                return pred_meta(z, r, p);
+            };
+            // band placement (SPEC.md §3.1)
+            off = 0;
+            if (np) {
+                const PredRow m0 = meta(p0);
+                int32_t bm = m0.rmax, barg = m0.rarg;
+                for (uint32_t s = 1; s < np; ++s) {
+                    const PredRow pm = meta(predp(s));
+                    if (pm.rmax > bm) bm = pm.rmax, barg = pm.rarg;
+                }
+                off = min(max(barg + 1 - kW / 2, 0), lim);
+            }
+            
+            // predecessor terms (SPEC.md §3.2)
+            int32_t Mh0 = kNeg, Mh1 = kNeg, Dv0 = kNeg, Dv1 = kNeg;
+            uint32_t ms0 = 0, ms1 = 0, ds0 = 0, ds1 = 0, dx0 = 0, dx1 = 0;
             for (uint32_t s = 0; s < np; ++s) {
                 const uint32_t p = predp(s);
                 const PredRow pm = meta(p);
@@ -401,89 +517,49 @@ __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_
                 {
                     const int a = hB + kO + kE, b = dB + kE;
                     const int c = b > a ? b : a;
-                    if (c > Dv0) Dv0 = c, ds0 = s, dx0 = b > a;
+                    if (c > Dv0) Dv0 = c, ds0 = s, dx0 = b > a ? 4u : 0u;
                 }
                 {
                     const int a = hC + kO + kE, b = dC + kE;
                     const int c = b > a ? b : a;
-                    if (c > Dv1) Dv1 = c, ds1 = s, dx1 = b > a;
+                    if (c > Dv1) Dv1 = c, ds1 = s, dx1 = b > a ? 4u : 0u;
                 }
             }
+            
+            if (off + kW <= (int32_t)m) o = row_cells<true>(z, S, r, off, m, base, Mh0, Mh1, Dv0, Dv1, dx0, dx1);
+            else o = row_cells<false>(z, S, r, off, m, base, Mh0, Mh1, Dv0, Dv1, dx0, dx1);
+            if (np > 1) {
+                // slots (SPEC.md §4 needs them); an MSRC cell's M slot is 0
+                const int32_t j0 = off + 2 * lane;
+                const bool ok0 = j0 < (int32_t)m, ok1 = j0 + 1 < (int32_t)m;
+                const uint32_t c0 = o.code & 15u, c1 = o.code >> 4;
+                const uint32_t s_m0 = ok0 && (c0 & 3u) != HC_MSRC ? ms0 : 0u;
+                const uint32_t s_m1 = ok1 && (c1 & 3u) != HC_MSRC ? ms1 : 0u;
+                const uint32_t s_d0 = ok0 ? ds0 : 0u, s_d1 = ok1 ? ds1 : 0u;
+                mi = S.nmulti - mi0;
+                st_slots[mi * 64 + lane] = s_m0 | (s_m1 << 8) | (s_d0 << 16) | (s_d1 << 24);
+                mi = S.nmulti++;
+            }
+            DP_STAMP(kPfRowB);  // general rows
         }
-        DP_STAMP(kPfRowB);
-        const int32_t j0 = off + t0, j1 = off + t1;
-        const bool v0 = j0 < (int32_t)m, v1 = j1 < (int32_t)m;
-        const uint32_t q0 = v0 ? rcode(z, (uint32_t)j0) : 0u;
-        const uint32_t q1 = v1 ? rcode(z, (uint32_t)j1) : 0u;
-        const int32_t src0 = j0 == 0 ? 0 : kO + kE * j0;
-        const int32_t src1 = kO + kE * j1;
-        uint32_t hc0, hc1;
-        int32_t mb0, mb1;
-        if (Mh0 >= src0) mb0 = Mh0, hc0 = HC_MPRED;
-        else mb0 = src0, hc0 = HC_MSRC, ms0 = 0;
-        if (Mh1 >= src1) mb1 = Mh1, hc1 = HC_MPRED;
-        else mb1 = src1, hc1 = HC_MSRC, ms1 = 0;
-        int32_t hp0 = mb0 + (base == q0 ? kMs : kXs);
-        int32_t hp1 = mb1 + (base == q1 ? kMs : kXs);
-        if (Dv0 > hp0) hp0 = Dv0, hc0 = HC_DEL;
-        if (Dv1 > hp1) hp1 = Dv1, hc1 = HC_DEL;
-        // in-row insertions (SPEC.md §3.4): exclusive prefix max of X = H' - E*t
-        const int32_t X0 = hp0 - kE * t0, X1 = hp1 - kE * t1;
-        const int32_t incl = wave_incl_max(max(X0, X1));
-        const int32_t Pex = wave_shr1(kNeg, incl);
-        const int32_t ex1 = max(Pex, X0);
-        const int32_t I0 = t0 == 0 ? kNeg : kO + kE * t0 + Pex;
-        const int32_t I1 = kO + kE * t1 + ex1;
-        const uint32_t iext1 = Pex > X0;
-        const uint32_t iext0 = (uint32_t)wave_shr1(0, (int)(ex1 > X1));
-        int32_t H0 = hp0, H1 = hp1;
-        if (I0 > H0) H0 = I0, hc0 = HC_INS;
-        if (I1 > H1) H1 = I1, hc1 = HC_INS;
-        uint32_t c0 = hc0 | (dx0 << 2) | (iext0 << 3);
-        uint32_t c1 = hc1 | (dx1 << 2) | (iext1 << 3);
-        if (!v0) H0 = kNeg, Dv0 = kNeg, c0 = 0, ms0 = 0, ds0 = 0;
-        if (!v1) H1 = kNeg, Dv1 = kNeg, c1 = 0, ms1 = 0, ds1 = 0;
-        DP_STAMP(kPfRowC);
-        // row max / argmax for the successors' band placement
-        const int32_t rm = wave_max(max(H0, H1));
-        const uint64_t hit0 = ballot(H0 == rm), hit1 = ballot(H1 == rm);
-        const uint32_t c0i = hit0 ? 2u * (uint32_t)__builtin_ctzll(hit0) : 256u;
-        const uint32_t c1i = hit1 ? 2u * (uint32_t)__builtin_ctzll(hit1) + 1u : 256u;
-        const int32_t rarg = off + (int32_t)(c0i < c1i ? c0i : c1i);
-        // free-end candidates (SPEC.md §3.5)
-        if (v0) {
-            const int32_t e = H0 + (j0 == (int32_t)m - 1 ? 0 : kO + kE * ((int32_t)m - 1 - j0));
-            if (e > S.bE) S.bE = e, S.bR = r, S.bJ = (uint32_t)j0;
-        }
-        if (v1) {
-            const int32_t e = H1 + (j1 == (int32_t)m - 1 ? 0 : kO + kE * ((int32_t)m - 1 - j1));
-            if (e > S.bE) S.bE = e, S.bR = r, S.bJ = (uint32_t)j1;
-        }
-        DP_STAMP(kPfRowD);
         // staged in LDS, flushed to HBM once per block
         const uint32_t i = r - r0;
-        st_codes[i * 64 + lane] = (uint8_t)(c0 | (c1 << 4));
-        uint32_t mi = kNone;
-        if (np > 1) {
-            mi = S.nmulti - mi0;
-            st_slots[mi * 64 + lane] = ms0 | (ms1 << 8) | (ds0 << 16) | (ds1 << 24);
-            mi = S.nmulti++;
-        }
+        st_codes[i * 64 + lane] = (uint8_t)o.code;
         if (lane == 0) {
             st_meta[i * 2] = off;
             st_meta[i * 2 + 1] = (int32_t)mi;
         }
         int32_t *row = z.lds + kLdsRing + (r % kRing) * 256;
-        row[lane] = H0;
-        row[64 + lane] = H1;
-        row[128 + lane] = Dv0;
-        row[192 + lane] = Dv1;
-        if (lane == 0) {
-            int32_t *mt = z.lds + kLdsMeta + (r % kRing) * 4;
-            mt[0] = off, mt[1] = rm, mt[2] = rarg;
-        }
-        spill_mask |= sp << i;
-        S.pH0 = H0, S.pH1 = H1, S.pD0 = Dv0, S.pD1 = Dv1, S.pOff = off, S.pRm = rm, S.pRarg = rarg;
+        row[lane] = o.H0;
+        row[64 + lane] = o.H1;
+        row[128 + lane] = o.D0;
+        row[192 + lane] = o.D1;
+        const bool mine = lane == (int)(r % kRing);
+        S.mOff = mine ? off : S.mOff;
+        S.mRm = mine ? o.rm : S.mRm;
+        S.mRarg = mine ? o.rarg : S.mRarg;
+        spill_mask |= ((info & kInfoSpill) ? 1u : 0u) << i;
+        S.pH0 = o.H0, S.pH1 = o.H1, S.pD0 = o.D0, S.pD1 = o.D1, S.pOff = off, S.pRm = o.rm, S.pRarg = o.rarg;
     }
     DP_STAMP(kPfRowE);
     const uint32_t nm = S.nmulti - mi0;
@@ -518,10 +594,12 @@ __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_
         }
         int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)S.nspill * (kW * 8 + 16));
         const int32_t *row = z.lds + kLdsRing + (r % kRing) * 256;
-        const int32_t *mt = z.lds + kLdsMeta + (r % kRing) * 4;
 #pragma unroll
         for (int q = 0; q < 4; ++q) rec[q * 64 + lane] = row[q * 64 + lane];
-        if (lane < 3) rec[256 + lane] = mt[lane];
+        const int l = (int)(r % kRing);
+        const int32_t mo = __builtin_amdgcn_readlane(S.mOff, l), mr = __builtin_amdgcn_readlane(S.mRm, l),
+                      ma = __builtin_amdgcn_readlane(S.mRarg, l);
+        if (lane == 0) rec[256] = mo, rec[257] = mr, rec[258] = ma;
         if (lane == 0) P<uint32_t>(z, z.L.sslot)[r] = S.nspill;
         ++S.nspill;
     }
@@ -530,8 +608,9 @@ __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_
 __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
 {
     DpState S;
-    S.bE = INT32_MIN, S.bR = 0, S.bJ = 0, S.nmulti = 0, S.nspill = 0;
+    S.bE = INT32_MIN, S.bKey = 0, S.nmulti = 0, S.nspill = 0;
     S.pH0 = S.pH1 = S.pD0 = S.pD1 = kNeg, S.pOff = 0, S.pRm = 0, S.pRarg = 0;
+    S.mOff = S.mRm = S.mRarg = 0;
     S.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.nxt = S.cur;
     FlushBuf fa, fb;
@@ -555,14 +634,18 @@ __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uin
     }
     pin(fa);
     pin(fb);
-    // lexicographic (max score, min row, min j) over the lanes' candidates
+    // lexicographic (max score, min row, min j) over the lanes' candidates;
+    // within one row a smaller lane (and t0 before t1) is a smaller j
     const int32_t best = wave_max(S.bE);
-    const uint32_t rsel = S.bE == best ? S.bR : 0x7FFFFFFFu;
+    const uint32_t rsel = S.bE == best ? S.bKey >> 1 : 0x7FFFFFFFu;
     const int32_t rmin = wave_min((int32_t)rsel);
-    const uint32_t jsel = (S.bE == best && S.bR == (uint32_t)rmin) ? S.bJ : 0x7FFFFFFFu;
-    const int32_t jmin = wave_min((int32_t)jsel);
+    const bool mine = S.bE == best && (S.bKey >> 1) == (uint32_t)rmin;
+    const uint32_t tsel = mine ? 2u * (uint32_t)threadIdx.x + (S.bKey & 1u) : 0x7FFFFFFFu;
+    const int32_t tmin = wave_min((int32_t)tsel);
     er_out = (uint32_t)rmin;
-    ej_out = (uint32_t)jmin;
+    __syncthreads();
+    const uint2 em = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin];  // flushed band offset of the end row
+    ej_out = em.x + (uint32_t)tmin;
     z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
     __syncthreads();
 }
@@ -655,32 +738,57 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             *reinterpret_cast<uint4 *>(tbs + o) = *reinterpret_cast<const uint4 *>(slots + (size_t)mi_lo * 256 + o);
         __syncthreads();
         DP_STAMP(kPfSpare0);
-        // lane 0 walks the block: per step one 16-B record read, one code
-        // byte, and for a multi-predecessor row one slot byte, all from LDS.
-        // Events are staged in LDS (a global store per step would stall the
-        // next step on its store-data wait) and flushed by the wave.
+        // The wave walks the block.  In state H a probe first follows the
+        // diagonal run in one go: lane i checks that cell (r - i, j - i) is
+        // MPRED and that its predecessor is row r - i - 1; the run ends at the
+        // first lane that fails.  Then one table-driven step (kTbAct) takes the
+        // cell where the run ended.  Events are staged in LDS (a global store
+        // per step would stall the next step on its store-data wait) and
+        // flushed by the wave.
         const int32_t jhi = j;
         uint32_t nev = 0, far_pred = kNone;
-        if (lane == 0) {
-            // branch-free step: a 6-bit index (state, 4-bit cell code) selects
-            // the step's action from kTbAct (see SPEC.md §4)
-            uint32_t rr = r, stt = (uint32_t)st, ne = 0, g = guard, fp = kNone;
+        {
+            uint32_t rr = r, stt = (uint32_t)st, ne = 0, g = guard;
             int32_t jj = j;
-            while (rr >= blo && ne < kEvStage) {
+            while (rr >= blo && ne + 65 <= kEvStage) {
                 if (++g > glim) {
                     err = kErrTrace;
                     done = 1;
                     break;
                 }
+                if (stt == 0) {
+                    const int32_t rowi = (int32_t)rr - (int32_t)lane, ji = jj - (int32_t)lane;
+                    bool ok = rowi >= (int32_t)blo && ji >= 0;
+                    const uint32_t ri = ok ? (uint32_t)rowi - blo : 0u;
+                    const uint4 rec = tbr[ri * 2];
+                    const uint32_t t = (uint32_t)ji - rec.x;
+                    ok = ok && t < (uint32_t)kW;
+                    const uint32_t tc = t & (uint32_t)(kW - 1);
+                    const uint32_t c = (tbc[ri * 64 + (tc >> 1)] >> ((tc & 1u) << 2)) & 15u;
+                    const uint32_t sl = rec.y != kNone ? tbs[rec.y * 256 + (tc >> 1) * 4 + (tc & 1u)] : 0u;
+                    const uint4 pp = tbr[ri * 2 + 1];
+                    const uint32_t prow = sl == 0 ? pp.x : sl == 1 ? pp.y : sl == 2 ? pp.z : pp.w;
+                    ok = ok && (c & 3u) == HC_MPRED && sl < 4 && prow + 1 == (uint32_t)rowi;
+                    const uint64_t bad = ~ballot(ok);
+                    const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+                    if (lane < k) evs[ne + lane] = (EV_ALN << 30) | (uint32_t)rowi;
+                    ne += k;
+                    rr -= k;
+                    jj -= (int32_t)k;
+                    if (rr < blo || rr == 0xFFFFFFFFu) break;
+                }
                 const uint32_t ri = rr - blo;
                 const uint4 rec = tbr[ri * 2];
                 const uint32_t t = (uint32_t)jj - rec.x;
-                const uint32_t c = (tbc[ri * 64 + (t >> 1)] >> ((t & 1u) << 2)) & 15u;
+                const uint32_t c = uni((uint32_t)(tbc[ri * 64 + (t >> 1)] >> ((t & 1u) << 2)) & 15u);
                 const uint64_t ta = stt == 0 ? kTbAct[0] : stt == 1 ? kTbAct[1] : kTbAct[2];
                 const uint64_t tn = stt == 0 ? kTbNext[0] : stt == 1 ? kTbNext[1] : kTbNext[2];
                 const uint32_t act = (uint32_t)(ta >> (c * 4)) & 15u;  // emit | pred | dj | stop
                 const uint32_t nst = (uint32_t)(tn >> (c * 4)) & 3u;
-                if (act & 1u) evs[ne++] = ((stt == 2 ? EV_INS : EV_ALN) << 30) | rr;
+                if (act & 1u) {
+                    if (lane == 0) evs[ne] = ((stt == 2 ? EV_INS : EV_ALN) << 30) | rr;
+                    ++ne;
+                }
                 if (act & 8u) {
                     lead_row = rr;
                     lead_j = (uint32_t)jj;
@@ -689,18 +797,20 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 }
                 jj -= (int32_t)((act >> 2) & 1u);
                 if (act & 2u) {
-                    const uint32_t s = rec.y != kNone ? tbs[rec.y * 256 + (t >> 1) * 4 + (stt == 1 ? 2u : 0u) + (t & 1u)] : 0u;
+                    const uint32_t s = rec.y != kNone
+                                           ? uni((uint32_t)tbs[rec.y * 256 + (t >> 1) * 4 + (stt == 1 ? 2u : 0u) + (t & 1u)])
+                                           : 0u;
                     if (s >= 4) {
-                        fp = rec.w + s;
+                        far_pred = rec.w + s;
                         stt = nst;
                         break;
                     }
                     const uint4 pp = tbr[ri * 2 + 1];
-                    rr = s == 0 ? pp.x : s == 1 ? pp.y : s == 2 ? pp.z : pp.w;
+                    rr = uni(s == 0 ? pp.x : s == 1 ? pp.y : s == 2 ? pp.z : pp.w);
                 }
                 stt = nst;
             }
-            r = rr, j = jj, st = (int32_t)stt, nev = ne, guard = g, far_pred = fp;
+            r = rr, j = jj, st = (int32_t)stt, nev = ne, guard = g;
         }
         DP_STAMP(kPfSpare1);
         r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
@@ -1143,8 +1253,10 @@ __device__ __forceinline__ void write_msa(Z &z, uint32_t ncols, uint32_t n, uint
 __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
 {
     extern __shared__ int32_t smem[];
-    const uint32_t zi = blockIdx.x;
-    if (zi >= a.nzmw) return;
+    if (blockIdx.x >= a.nzmw) return;
+    // longest-processing-time-first: the host orders the batch by cost so the
+    // largest ZMWs start first and the tail of the launch is short ones
+    const uint32_t zi = a.order[blockIdx.x];
     const uint32_t lane = threadIdx.x;
     Z z;
     z.d = a.desc[zi];

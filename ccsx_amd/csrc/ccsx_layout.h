@@ -127,6 +127,7 @@ struct KArgs {
     const uint32_t *soff;  // segment offset relative to the ZMW's seq_off
     const uint32_t *slen;
     const ZmwDesc *desc;
+    const uint32_t *order;  // workgroup -> ZMW index: most expensive first (host-sorted)
     uint8_t *ws;
     uint8_t *out;
     uint8_t *msa;

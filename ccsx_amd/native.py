@@ -269,7 +269,7 @@ class Engine:
         return self.fetch()
 
     PROF_SLOTS = ("total", "load_read", "dp", "traceback", "merge", "columns", "shred", "dp_rows",
-                  "row_A_place", "row_B_preds", "row_C_cells", "row_D_rowmax", "row_E_store", "flush", "spare0", "spare1")
+                  "row_A_fast", "row_B_general", "row_C_unused", "row_D_nfast", "row_E_store_loop", "flush", "spare0", "spare1")
 
     def set_profiling(self, on: bool = True) -> None:
         self._L.ccsx_gpu_set_profiling(self._ctx, 1 if on else 0)
