@@ -62,6 +62,8 @@ struct ccsx_ctx {
     uint32_t nseg_total = 0;
     std::vector<ccsx::ZmwDesc> desc;
     bool profiling = false;
+    uint32_t tight_rows = 0;           // test hook: override the tight row cap
+    std::vector<uint8_t> run_arena;    // ccsx_gpu_run's gathered CCS strings
     DevBuf d_prof;
     std::vector<unsigned long long> h_prof;
     DevBuf d_seq, d_soff, d_slen, d_desc, d_order, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
@@ -145,8 +147,32 @@ const char *ccsx_gpu_status_str(int32_t s)
     }
 }
 
-// internal: stage with an optional MSA slab per ZMW (single-POA mode)
-int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa)
+static void zmw_extent(const ccsx_zmw_in &zi, uint64_t &S, uint64_t &hi, uint32_t &lmax)
+{
+    S = 0, hi = 0, lmax = 0;
+    for (uint32_t k = 0; k < zi.nseg; ++k) {
+        S += zi.seg_len[k];
+        lmax = std::max(lmax, zi.seg_len[k]);
+        hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
+    }
+}
+
+// device bytes one ZMW occupies when staged
+static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, uint32_t tight_rows)
+{
+    uint64_t S, hi;
+    uint32_t lmax;
+    zmw_extent(zi, S, hi, lmax);
+    ccsx::ZmwDesc d{};
+    ccsx::zcaps(d, S, lmax, zi.nseg, full, tight_rows);
+    ccsx::ZLayout L;
+    ccsx::zlayout(L, d);
+    return ccsx::align256(L.total) + hi + d.outcap + uint64_t(zi.nseg) * 8 + sizeof(ccsx::ZmwDesc) + 32;
+}
+
+// internal: stage with an optional MSA slab per ZMW (single-POA mode) and
+// full (exact upper bound) or tight capacities (ccsx_layout.h:zcaps)
+int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa, int full_caps)
 {
     if (!c) return -1;
     HIPCHK(c, hipSetDevice(c->device));
@@ -156,19 +182,15 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     uint32_t nseg = 0, lmax_all = 0, nmax = 0;
     for (size_t i = 0; i < nz; ++i) {
         const ccsx_zmw_in &zi = z[i];
-        uint64_t S = 0, hi = 0;
-        uint32_t lmax = 0;
-        for (uint32_t k = 0; k < zi.nseg; ++k) {
-            S += zi.seg_len[k];
-            lmax = std::max(lmax, zi.seg_len[k]);
-            hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
-        }
+        uint64_t S, hi;
+        uint32_t lmax;
+        zmw_extent(zi, S, hi, lmax);
         if (S + zi.nseg + 64 > 0x3FFFFFFFull) {
             c->err = "ZMW too large (sum of segment lengths >= 2^30)";
             return -1;
         }
         ccsx::ZmwDesc &d = c->desc[i];
-        ccsx::zcaps(d, S, lmax, zi.nseg);
+        ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows);
         d.seg0 = nseg;
         d.seq_off = seq_b;
         seq_b += hi;
@@ -242,7 +264,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     return 0;
 }
 
-int ccsx_gpu_stage(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz) { return ccsx_gpu_stage_ex(c, z, nz, 0); }
+int ccsx_gpu_stage(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz) { return ccsx_gpu_stage_ex(c, z, nz, 0, 0); }
 
 int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
 {
@@ -331,13 +353,90 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
     return bad ? -2 : 0;
 }
 
+static bool is_cap_error(int32_t s)
+{
+    return s == ccsx::kErrRows || s == ccsx::kErrEdges || s == ccsx::kErrMulti || s == ccsx::kErrSpill;
+}
+
+// One chunk.  The chunk is cut into slices that fit the device's free memory
+// (tight caps); a ZMW that outgrows a tight cap is re-run with full caps.
 int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out)
 {
-    int r = ccsx_gpu_stage(c, z, nz);
+    if (!c) return -1;
+    if (mode != CCSX_MODE_SHRED && mode != CCSX_MODE_PRIMITIVE) {
+        c->err = "mode must be CCSX_MODE_SHRED or CCSX_MODE_PRIMITIVE";
+        return -1;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    size_t freeb = 0, totb = 0;
+    HIPCHK(c, hipMemGetInfo(&freeb, &totb));
+    const uint64_t held = c->d_ws.cap + c->d_seq.cap + c->d_out.cap + c->d_msa.cap;
+    const uint64_t budget = freeb + held > (3ull << 30) ? freeb + held - (3ull << 30) : (1ull << 30);
+    c->run_arena.clear();
+    std::vector<uint64_t> aoff(nz, 0);
+    std::string first_err;
+    auto run_list = [&](const std::vector<uint32_t> &idx, bool full, std::vector<uint32_t> *retry) -> int {
+        size_t b = 0;
+        while (b < idx.size()) {
+            uint64_t need = 0;
+            size_t e = b;
+            while (e < idx.size()) {
+                const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows);
+                if (e > b && need + x > budget) break;
+                need += x;
+                ++e;
+            }
+            std::vector<ccsx_zmw_in> sub(e - b);
+            for (size_t i = b; i < e; ++i) sub[i - b] = z[idx[i]];
+            int r = ccsx_gpu_stage_ex(c, sub.data(), sub.size(), 0, full ? 1 : 0);
+            if (r) return r;
+            r = ccsx_gpu_launch_ex(c, mode, nullptr);
+            if (r) return r;
+            std::vector<ccsx_zmw_out> o(sub.size());
+            r = ccsx_gpu_fetch(c, o.data());
+            if (r && r != -2) return r;
+            for (size_t i = 0; i < sub.size(); ++i) {
+                const uint32_t g = idx[b + i];
+                out[g].cells = o[i].cells;
+                out[g].status = o[i].status;
+                out[g].len = 0;
+                if (o[i].status) {
+                    if (retry && is_cap_error(o[i].status)) {
+                        retry->push_back(g);
+                    } else if (first_err.empty()) {
+                        char m[200];
+                        snprintf(m, sizeof m, "ZMW %u of the batch failed on the device: %s", g,
+                                 ccsx_gpu_status_str(o[i].status));
+                        first_err = m;
+                    }
+                    continue;
+                }
+                aoff[g] = c->run_arena.size();
+                out[g].len = o[i].len;
+                c->run_arena.insert(c->run_arena.end(), o[i].ccs, o[i].ccs + o[i].len);
+            }
+            b = e;
+        }
+        return 0;
+    };
+    std::vector<uint32_t> all(nz), retry;
+    for (size_t i = 0; i < nz; ++i) all[i] = uint32_t(i);
+    int r = run_list(all, false, &retry);
+    if (!r && !retry.empty()) r = run_list(retry, true, nullptr);
     if (r) return r;
-    r = ccsx_gpu_launch(c, mode, nullptr);
-    if (r) return r;
-    return ccsx_gpu_fetch(c, out);
+    for (size_t i = 0; i < nz; ++i) out[i].ccs = reinterpret_cast<const char *>(c->run_arena.data() + aoff[i]);
+    if (!first_err.empty()) {
+        c->err = first_err;
+        return -2;
+    }
+    return 0;
+}
+
+int ccsx_gpu_set_tight_rows(ccsx_ctx *c, uint32_t rows)
+{
+    if (!c) return -1;
+    c->tight_rows = rows;
+    return 0;
 }
 
 int ccsx_gpu_set_profiling(ccsx_ctx *c, int on)
@@ -369,7 +468,7 @@ uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *c)
 int ccsx_gpu_single_poa(ccsx_ctx *c, const ccsx_zmw_in *z, const uint8_t **cns, uint32_t *ncns,
                         const uint8_t **msa, uint32_t *ncols)
 {
-    int r = ccsx_gpu_stage_ex(c, z, 1, 1);
+    int r = ccsx_gpu_stage_ex(c, z, 1, 1, 1);
     if (r) return r;
     r = ccsx_gpu_launch_ex(c, ccsx::kSinglePoa, nullptr);
     if (r) return r;

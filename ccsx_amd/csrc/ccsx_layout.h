@@ -107,17 +107,31 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 }
 
 // Capacities for a ZMW with segment lengths summing to S, longest segment
-// lmax, n segments.  Rows and edges are exact upper bounds (SPEC.md §5: each
-// read base creates at most one node and one in-edge); mcap/scap are sized
-// generously and checked at run time (kErrMulti / kErrSpill).
-CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n)
+// lmax, n segments.  Full caps are exact upper bounds for rows and edges
+// (SPEC.md §5: each read base creates at most one node and one in-edge).
+// Tight caps (the default launch) size the DP/graph arrays for the graphs a
+// ZMW really builds -- rows ~ window length x (1 + error rate x reads) -- at
+// a fraction of the memory; every cap is checked on the device (kErrRows,
+// kErrEdges, kErrMulti, kErrSpill) and ccsx_gpu_run re-runs a ZMW that hits
+// one with full caps.  tight_rows overrides the tight row cap (tests).
+CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, bool full = true,
+                          uint32_t tight_rows = 0)
 {
     d.n = n;
     d.rcap = uint32_t(S + 16);
     d.ecap = uint32_t(S + n + 16);
-    d.lcap = lmax + 16;
     d.mcap = d.rcap / 2 + 64;
     d.scap = d.rcap / 4 + 64;
+    if (!full) {
+        uint64_t r = tight_rows ? tight_rows : 3ull * lmax + 4096;
+        if (r < S) {
+            d.rcap = uint32_t(r + 16);
+            d.ecap = 2 * d.rcap;
+        }
+        d.mcap = d.rcap / 4 + 64;
+        d.scap = d.rcap / 32 + 64;
+    }
+    d.lcap = lmax + 16;
     d.nw = (n + 63) / 64 ? (n + 63) / 64 : 1;
     d.outcap = uint32_t(S + 16);
 }

@@ -23,7 +23,7 @@ MODE_PRIMITIVE = 1
 EXPORTS = {
     "ccsx_gpu.h": ["ccsx_gpu_device_count", "ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
-                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile"],
+                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_set_tight_rows"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw"],
     "ccsx_seqio.h": ["ccsx_reader_open", "ccsx_reader_next", "ccsx_reader_close"],
@@ -66,6 +66,7 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_staged_bytes.restype = C.c_uint64
         L.ccsx_gpu_set_profiling.argtypes = [C.c_void_p, C.c_int]
         L.ccsx_gpu_profile.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]
+        L.ccsx_gpu_set_tight_rows.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_revcomp.argtypes = [C.c_char_p, C.c_uint32]
         L.ccsx_prepare.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]
@@ -263,10 +264,18 @@ class Engine:
         return res
 
     def run(self, zmws: list[Prepared], mode: int = MODE_SHRED):
-        """stage + launch + fetch: returns [(ccs bytes, status, cells)]."""
-        self.stage(zmws)
-        self.launch(mode)
-        return self.fetch()
+        """ccsx_gpu_run (memory-sized slices, full-capacity re-run of ZMWs that
+        outgrow the tight workspace): returns [(ccs bytes, status, cells)]."""
+        arr, keep = self._build_in(zmws)
+        out = (ZmwOut * max(len(zmws), 1))()
+        if self._L.ccsx_gpu_run(self._ctx, mode, arr, len(zmws), out) != 0:
+            self._err("ccsx_gpu_run")
+        return [(C.string_at(out[i].ccs, out[i].len) if out[i].len else b"", out[i].status, out[i].cells)
+                for i in range(len(zmws))]
+
+    def set_tight_rows(self, rows: int) -> None:
+        """Test hook: override the tight row capacity (0 = default)."""
+        self._L.ccsx_gpu_set_tight_rows(self._ctx, rows)
 
     PROF_SLOTS = ("total", "load_read", "dp", "traceback", "merge", "columns", "shred", "dp_rows",
                   "row_A_fast", "row_B_general", "row_C_unused", "row_D_nfast", "row_E_store_loop", "flush", "spare0", "spare1")

@@ -58,12 +58,15 @@ void ccsx_gpu_close(ccsx_ctx *ctx);
 const char *ccsx_gpu_error(const ccsx_ctx *ctx);
 const char *ccsx_gpu_status_str(int32_t status);
 
-/* One chunk: stage + launch + fetch (replaces kt_for(ccs_for2/ccs_for)). */
+/* One chunk (replaces kt_for(ccs_for2/ccs_for)): stage + launch + fetch, in
+ * slices that fit the device memory; a ZMW whose graph outgrows the default
+ * (tight) workspace capacities is re-run with exact upper-bound capacities. */
 int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out);
 
-/* The same in three steps, so inputs can stay resident in HBM across launches
- * (used by bench.py).  ccsx_gpu_launch returns the kernel time measured with
- * HIP events on the context's stream. */
+/* The same in three steps (one slice, tight capacities, no re-run), so inputs
+ * can stay resident in HBM across launches (used by bench.py).
+ * ccsx_gpu_launch returns the kernel time measured with HIP events on the
+ * context's stream. */
 int ccsx_gpu_stage(ccsx_ctx *ctx, const ccsx_zmw_in *z, size_t nz);
 int ccsx_gpu_launch(ccsx_ctx *ctx, int mode, float *kernel_ms);
 int ccsx_gpu_fetch(ccsx_ctx *ctx, ccsx_zmw_out *out);
@@ -75,6 +78,8 @@ uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *ctx);
  * ZMWs of the last launch: total, read staging, DP, traceback, merge,
  * columns, breakpoint+emission, DP rows.  Off by default. */
 int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
+/* Test hook: tight row capacity override (0 = default 3 x longest segment + 4096). */
+int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
 int ccsx_gpu_profile(ccsx_ctx *ctx, uint64_t *sums, uint32_t nslots);
 
 #ifdef __cplusplus

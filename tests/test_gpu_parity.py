@@ -88,3 +88,29 @@ def test_gpu_full_size_properties(engine):
     want, _, _ = batch([zs[i] for i in sample], cx.MODE_SHRED, 6)
     for i, w in zip(sample, want):
         assert got[i][0] == w
+
+
+@pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
+def test_capacity_rerun(engine, mode):
+    """A ZMW whose graph outgrows the tight workspace is re-run with full caps
+    (ccsx_gpu_run) and still matches the oracle; a tiny tight row cap forces
+    the re-run for every ZMW of the batch but one tiny one."""
+    zs = [synth(h, 3000, 6) for h in range(5)] + [cx.prepare([b"ACGTACGTAC"] * 5)]
+    engine.set_tight_rows(600)
+    try:
+        _check(engine, zs, mode)
+    finally:
+        engine.set_tight_rows(0)
+
+
+def test_tight_caps_fail_loudly_without_rerun(engine):
+    """stage/launch/fetch (no re-run) reports the capacity status."""
+    zs = [synth(h, 3000, 6) for h in range(2)]
+    engine.set_tight_rows(600)
+    try:
+        engine.stage(zs)
+        engine.launch(cx.MODE_SHRED)
+        with pytest.raises(cx.GpuError):
+            engine.fetch()
+    finally:
+        engine.set_tight_rows(0)
