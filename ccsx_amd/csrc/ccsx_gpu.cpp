@@ -209,7 +209,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     }
     c->seq_bytes = seq_b, c->ws_bytes = ws_b, c->out_bytes = out_b, c->msa_bytes = msa_b;
     c->nseg_total = nseg;
-    c->lds_read_words = (lmax_all + 15) / 16 + 1;
+    c->lds_read_words = (lmax_all + 7) / 8 + 2;  // nibble-pair read buffer (ccsx_kernel.hip load_read)
     c->lds_nmax = std::max<uint32_t>(nmax, 1);
     size_t freeb = 0, totb = 0;
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));

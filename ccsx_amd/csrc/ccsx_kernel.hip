@@ -97,9 +97,33 @@ __device__ __forceinline__ int wave_incl_sum(int v)
     return v;
 }
 
+// lane within the wave; the workgroup is two waves (wave 0 runs every phase,
+// wave 1 is the DP helper, see dp_align)
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// Visibility point for single-wave phases: LDS and global accesses of the
+// wave before it are complete (the workgroup barrier is reserved for the
+// two-wave DP protocol, which both waves must enter the same number of times)
+__device__ __forceinline__ void wsync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
+
+// Workgroup barrier for the two-wave DP's block handoff: only LDS must be
+// complete (__syncthreads would also drain wave 1's in-flight HBM stores)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old, v); }  // lane l <- l-1
 
 __device__ __forceinline__ int wave_shl1(int old, int v) { return dpp<0x130>(old, v); }  // lane l <- l+1
+
+// lane `l` of v <- the uniform value x (v_writelane_b32; l and x in SGPRs)
+__device__ __forceinline__ int writelane(int v, int x, int l)
+{
+    // gfx9 VOP3 reads one SGPR: the lane select goes through m0
+    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
+                 : "+v"(v)
+                 : "s"(__builtin_amdgcn_readfirstlane(x)), "s"(__builtin_amdgcn_readfirstlane(l))
+                 : "m0");
+    return v;
+}
 
 __device__ __forceinline__ int wave_max(int v) { return __builtin_amdgcn_readlane(wave_incl_max(v), 63); }
 
@@ -135,7 +159,7 @@ struct Z {
     const uint8_t *seq;
     int32_t *lds;        // ring: kRing * 256 ints
     int32_t *meta;       // kRing * 4 ints: off, rmax, rarg, tof
-    uint32_t *rd;        // packed 2-bit read codes
+    uint8_t *rd;         // read as nibble pairs: byte b = pair(2b) | pair(2b+1) << 4, pair(j) = code(j) | code(j+1) << 2
     uint32_t *pos;       // shredding cursors
     uint32_t rdcap;      // bases that fit in rd
     int cur;
@@ -147,6 +171,17 @@ struct Z {
 };
 
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
+
+// Raw buffer access: lanes whose byte offset is >= `bytes` are discarded
+// (stores) or read 0 (loads) by the hardware, so a masked store is still one
+// unconditionally issued instruction -- the compiler's vmcnt bookkeeping stays
+// exact and a later wait on a prefetch never waits on these stores.
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
 
 // Diagnostic build only (-DCCSX_DP_STAMPS, libccsx_amd_diag.so): shader-clock
 // stamps between the phases of one DP row; never compiled into the product.
@@ -178,26 +213,32 @@ __device__ __forceinline__ uint64_t *G_mem(const Z &z, int b) { return P<uint64_
 __device__ __forceinline__ uint32_t *G_poff(const Z &z, int b) { return P<uint32_t>(z, b ? z.L.poff1 : z.L.poff0); }
 __device__ __forceinline__ uint32_t *G_pred(const Z &z, int b) { return P<uint32_t>(z, b ? z.L.pred1 : z.L.pred0); }
 
-__device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return (z.rd[j >> 4] >> ((j & 15u) * 2u)) & 3u; }
+__device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return ((uint32_t)z.rd[j >> 1] >> ((j & 1u) * 4u)) & 3u; }
 
 // ----------------------------------------------------------------------------
-// push: stage read k (ASCII in HBM) into LDS as 2-bit codes
+// push: stage read k (ASCII in HBM) into LDS as nibble pairs: the byte at
+// (off >> 1) + l holds, in nibble off & 1, the codes of read positions
+// off + 2l and off + 2l + 1 -- one ds_read_u8 per lane per DP row
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
 {
-    const uint32_t lane = threadIdx.x;
-    const uint32_t nwd = (m + 15) / 16;
+    const uint32_t lane = lane_id();
+    const uint32_t nwd = (m + 7) / 8 + 1;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(z.rd);
     for (uint32_t w = lane; w < nwd; w += 64) {
+        uint32_t c[9];
+#pragma unroll
+        for (uint32_t b = 0; b < 9; ++b) {
+            const uint32_t j = w * 8 + b;
+            c[b] = j < m ? enc_base(src[j]) : 0u;
+        }
         uint32_t x = 0;
 #pragma unroll
-        for (uint32_t b = 0; b < 16; ++b) {
-            const uint32_t j = w * 16 + b;
-            const uint32_t c = j < m ? enc_base(src[j]) : 0u;
-            x |= c << (2 * b);
-        }
-        z.rd[w] = x;
+        for (uint32_t k = 0; k < 4; ++k)
+            x |= (c[2 * k] | c[2 * k + 1] << 2 | c[2 * k + 1] << 4 | c[2 * k + 2] << 6) << (8 * k);
+        dst[w] = x;
     }
-    __syncthreads();
+    wsync();
 }
 
 // read the two cells of lane l at band index 2l+c (c wave-uniform) from a row
@@ -223,14 +264,18 @@ struct PredRow {
 };
 
 // LDS layout of one wave (int32 words)
-constexpr int kLdsRing = 0;                          // kRing rows x [Hev|Hod|Dev|Dod] x 64
-constexpr int kLdsMeta = kRing * 256;                // (spare) kRing x 4 words
+constexpr int kLdsRing = 0;                          // kRing rows: [Hev|Hod|Dev|Dod] x 64 (dp_block) or kRowW (dp_fast)
+constexpr int kLdsMeta = kRingA * kRowW;             // (spare) kRing x 4 words
 constexpr int kLdsStCodes = kLdsMeta + kRing * 4;    // kBlk rows x 64 B of codes
 constexpr int kBlk = 16;                             // rows per flush block
 constexpr int kLdsStMeta = kLdsStCodes + kBlk * 16;  // kBlk x {off, mi}
 constexpr int kLdsStSlots = kLdsStMeta + kBlk * 2;   // kBlk x 256 B of slots
-constexpr int kLdsFixed = kLdsStSlots + kBlk * 64;   // then: packed read codes, shredding cursors
+constexpr int kLdsPub = kLdsStSlots + kBlk * 64;     // kPubSlots x {M0, M1, Pex} x 64: wave 0 -> wave 1
+constexpr int kLdsOffRing = kLdsPub + kPubSlots * 192;  // 64: band offset of DP row q at q & 63
+constexpr int kLdsJob = kLdsOffRing + 64;             // 16: two-wave DP job / results
+constexpr int kLdsFixed = kLdsJob + 16;               // then: the read (nibble pairs), shredding cursors
 static_assert(kBlk == kRing, "the ring doubles as the spill source of a flushed block");
+
 static_assert(kLdsFixed == kLdsFixedWords, "host and device LDS layouts disagree");
 
 // meta of a spilled row (rows within the ring keep theirs in registers, DpState)
@@ -271,7 +316,10 @@ __device__ __forceinline__ void pin(FlushBuf &f)
 struct RowPre {
     uint32_t info, po, p0, p1, p2, p3;
 };
-constexpr uint32_t kInfoSpill = 4u, kInfoChain = 8u;
+// row info bits: base (0-1) | spill (2: a successor lies > kRing rows ahead)
+// | chain (3: the only predecessor is the previous row) | far (4: a
+// predecessor lies > kRing rows back or there are > 4) | np << 8
+constexpr uint32_t kInfoSpill = 4u, kInfoChain = 8u, kInfoFar = 16u;
 
 struct DpState {
     int32_t bE;
@@ -285,7 +333,7 @@ struct DpState {
 
 __device__ __forceinline__ void prefetch_rows(const Z &z, uint32_t r0, RowPre &o)
 {
-    const uint32_t rr = r0 + threadIdx.x;
+    const uint32_t rr = r0 + lane_id();
     if (rr < z.R) {
         const uint8_t *nb = G_nb(z, z.cur);
         const uint32_t *poff = G_poff(z, z.cur);
@@ -301,6 +349,17 @@ __device__ __forceinline__ void prefetch_rows(const Z &z, uint32_t r0, RowPre &o
     }
 }
 
+// dp_fast: one coalesced record per row, written by merge (no dependent loads)
+__device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o)
+{
+    const uint32_t n = r0 < z.R ? z.R - r0 : 0u;
+    const v4u q = __builtin_amdgcn_raw_buffer_load_b128(brsrc(P<const uint4>(z, z.L.rrec) + r0, n * 16),
+                                                        lane_id() * 16, 0, 0);
+    const uint32_t sp = __builtin_amdgcn_raw_buffer_load_b8(brsrc(P<const uint8_t>(z, z.L.spf) + r0, n), lane_id(), 0, 0);
+    o.info = q.x | (sp ? kInfoSpill : 0u), o.p0 = q.y, o.p1 = q.z, o.p2 = q.w;
+    o.p3 = __builtin_amdgcn_raw_buffer_load_b32(brsrc(P<const uint32_t>(z, z.L.rp3) + r0, n * 4), lane_id() * 4, 0, 0);
+}
+
 // The cells of one row given the predecessor terms (SPEC.md §3.2-§3.5).
 // hA = max_s Hp_s(j0-1) (= Mh of t0), hB = Mh of t1, Dv0/Dv1 and their slot /
 // ext bits computed by the caller.  FULL: every cell of the band is valid.
@@ -314,14 +373,12 @@ __device__ __forceinline__ RowOut row_cells(const Z &z, DpState &S, uint32_t r, 
                                             int32_t Mh0, int32_t Mh1, int32_t Dv0, int32_t Dv1, uint32_t dx0,
                                             uint32_t dx1)
 {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int32_t t0 = 2 * lane;
     const int32_t j0 = off + t0, j1 = j0 + 1;
-    // read codes of the two cells: one ds_read2 of the packed read
-    const uint32_t w = (uint32_t)j0 >> 4;
-    const uint64_t wd = (uint64_t)z.rd[w] | ((uint64_t)z.rd[w + 1] << 32);
-    const uint32_t sh = ((uint32_t)j0 & 15u) * 2u;
-    const uint32_t q0 = (uint32_t)(wd >> sh) & 3u, q1 = (uint32_t)(wd >> (sh + 2)) & 3u;
+    // read codes of the two cells: one nibble pair
+    const uint32_t qp = (uint32_t)z.rd[(uint32_t)j0 >> 1] >> (((uint32_t)j0 & 1u) * 4u);
+    const uint32_t q0 = qp & 3u, q1 = (qp >> 2) & 3u;
     // M (SPEC.md §3.2)
     int32_t src0 = kO + kE * j0;
     if (off == 0) src0 = lane == 0 ? 0 : src0;
@@ -392,7 +449,7 @@ __device__ __forceinline__ RowOut row_cells(const Z &z, DpState &S, uint32_t r, 
 template <bool SLOW>
 __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_t m, FlushBuf &f)
 {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const uint32_t R = z.R;
     const uint32_t r0 = blk * kBlk;
     if (r0 >= R) return;
@@ -605,8 +662,707 @@ __device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_
     }
 }
 
+// ----------------------------------------------------------------------------
+// SPEC.md §3 on two waves.  One wave alone issues about one instruction per
+// 6 clocks whatever else runs on its SIMD (tools/ubench/issue.hip), and a
+// batch of ~1,000 ZMWs puts ~1 wave on each of the 1,024 SIMDs, so the DP of
+// one ZMW is split across the two waves of its workgroup:
+//  * wave 0 ("A") runs the recurrence: band placement, M / D / H', the
+//    insertion prefix-max and row-max scans, H; it writes each row's H and D
+//    to an LDS ring of kRingA rows, the exclusive prefix max (Pex) of the
+//    row's insertion scan and the row's band offset;
+//  * wave 1 ("B") follows one block of kBlkAB rows behind: from the ring it
+//    recomputes every cell's decision bits (SPEC.md §3.2-§3.4: MPRED / MSRC /
+//    DEL / INS, D-ext, I-ext), the predecessor slots of multi-predecessor
+//    rows and the free-end candidates, stages them and flushes them to HBM.
+// The waves meet at one workgroup barrier per block.  Everything else in the
+// kernel runs on wave 0 alone; wave 1 waits in dp_helper for the next DP.
+//
+// Value-preserving choices (the oracle is followed bit for bit):
+//  * ring row = [pad4 | H x 128 | pad4][pad4 | D x 128 | pad4]; pads hold
+//    kNegH = kNeg + 5 (H) and kNeg (D), so a predecessor at any band shift in
+//    [-3, 4] is three DS reads with immediate offsets, and
+//    D = max(H + O + E, D + E) needs no kNeg floor (an out-of-band H then
+//    contributes exactly kNeg, which never wins a strict > update);
+//  * row max and its first position come from one max-scan of
+//    key = H' << 7 | (127 - t) (valid H' lies in (-2^24, 2^24) for m < 2^22),
+//    and max H == max H' at the same first position (an insertion value is
+//    always below the H' it extends);
+//  * free-end candidates are tracked on H' for the same reason.
+// ----------------------------------------------------------------------------
+constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
+constexpr int32_t kNegH = kNeg - kO - kE;
+constexpr int kBlkAB = 2;  // rows per A/B lockstep block
+static_assert(kPubSlots >= 2 * kBlkAB, "wave 1 reads the block before wave 0's");
+static_assert(kRingA * kRowW >= kRing * 256, "ring area too small for dp_block");
+static_assert(kRingA >= kRing + 2 * kBlkAB, "B reads predecessors up to kRing rows behind its row");
+
+static_assert(kLdsRing + kRingA * kRowW <= kLdsMeta, "ring overlaps the meta area");
+
+enum JobKind : int32_t { kJobExit = 0, kJobDp = 1 };
+struct DpJob {
+    int32_t kind;
+    uint32_t m, R, cur;
+    // results (B)
+    uint32_t er, ej, nmulti;
+    int32_t status;
+};
+
+__device__ __forceinline__ volatile DpJob *dp_job(const Z &z)
+{
+    return reinterpret_cast<volatile DpJob *>(z.lds + kLdsJob);
+}
+
+// fold predecessor slot s's five cells into the running Mh / D terms
+struct PredAcc {
+    int32_t Mh0, Mh1, Dv0, Dv1;
+    uint32_t ms0, ms1, ds0, ds1, dx0, dx1;
+};
+
+template <bool SLOTS>
+__device__ __forceinline__ void pred_fold(PredAcc &A, uint32_t s, int32_t hA, int32_t hB, int32_t hC, int32_t dB,
+                                          int32_t dC)
+{
+    const int32_t a0 = hB + (kO + kE), b0 = dB + kE, a1 = hC + (kO + kE), b1 = dC + kE;
+    const int32_t c0 = max(a0, b0), c1 = max(a1, b1);
+    if (s == 0) {
+        A.Mh0 = hA, A.Mh1 = hB, A.Dv0 = c0, A.Dv1 = c1;
+        if (SLOTS) {
+            A.ms0 = 0, A.ms1 = 0, A.ds0 = 0, A.ds1 = 0;
+            A.dx0 = b0 > a0 ? 4u : 0u;
+            A.dx1 = b1 > a1 ? 4u : 0u;
+        }
+    } else if (!SLOTS) {
+        A.Mh0 = max(A.Mh0, hA), A.Mh1 = max(A.Mh1, hB), A.Dv0 = max(A.Dv0, c0), A.Dv1 = max(A.Dv1, c1);
+    } else {
+        if (hA > A.Mh0) A.Mh0 = hA, A.ms0 = s;
+        if (hB > A.Mh1) A.Mh1 = hB, A.ms1 = s;
+        if (c0 > A.Dv0) A.Dv0 = c0, A.ds0 = s, A.dx0 = b0 > a0 ? 4u : 0u;
+        if (c1 > A.Dv1) A.Dv1 = c1, A.ds1 = s, A.dx1 = b1 > a1 ? 4u : 0u;
+    }
+}
+
+// the five cells of a predecessor row at band shift sh (lane's cells 2l, 2l+1)
+__device__ __forceinline__ void pred_cells(const int32_t *row, int32_t sh, int lane, int32_t &hA, int32_t &hB,
+                                           int32_t &hC, int32_t &dB, int32_t &dC)
+{
+    if ((uint32_t)(sh + 3) <= 7u) {
+        const int32_t *b = row + kHc - 1 + 2 * lane + sh;
+        hA = b[0];
+        hB = b[1];
+        hC = b[2];
+        dB = b[kDc - kHc + 1];
+        dC = b[kDc - kHc + 2];
+    } else {
+        const int32_t i = 2 * lane + sh;
+        hA = (uint32_t)(i - 1) < (uint32_t)kW ? row[kHc + i - 1] : kNegH;
+        hB = (uint32_t)i < (uint32_t)kW ? row[kHc + i] : kNegH;
+        hC = (uint32_t)(i + 1) < (uint32_t)kW ? row[kHc + i + 1] : kNegH;
+        dB = (uint32_t)i < (uint32_t)kW ? row[kDc + i] : kNeg;
+        dC = (uint32_t)(i + 1) < (uint32_t)kW ? row[kDc + i + 1] : kNeg;
+    }
+}
+
+// the predecessor terms of row r (np <= 4, every predecessor in the ring)
+template <bool SLOTS>
+__device__ __forceinline__ void pred_terms(const int32_t *ring, int32_t off, uint32_t np, uint32_t p0, uint32_t p1,
+                                           uint32_t p2, uint32_t p3, int32_t o0, int32_t o1, int32_t o2, int32_t o3,
+                                           int lane, PredAcc &A)
+{
+    const int32_t s0 = off - o0, s1 = off - o1, s2 = off - o2, s3 = off - o3;
+    const bool inr = (uint32_t)(s0 + 3) <= 7u && (np < 2 || (uint32_t)(s1 + 3) <= 7u) &&
+                     (np < 3 || (uint32_t)(s2 + 3) <= 7u) && (np < 4 || (uint32_t)(s3 + 3) <= 7u);
+    if (np == 0) {
+        pred_fold<SLOTS>(A, 0, kNegH, kNegH, kNegH, kNeg, kNeg);
+    } else if (inr) {
+        // every predecessor within the padded band: issue all reads (absent
+        // slots re-read slot 0's row), then fold
+        const int L2 = 2 * lane;
+        const int32_t *b0 = ring + (p0 % kRingA) * kRowW + (kHc - 1) + L2 + s0;
+        const int32_t *b1 = np > 1 ? ring + (p1 % kRingA) * kRowW + (kHc - 1) + L2 + s1 : b0;
+        const int32_t *b2 = np > 2 ? ring + (p2 % kRingA) * kRowW + (kHc - 1) + L2 + s2 : b0;
+        const int32_t *b3 = np > 3 ? ring + (p3 % kRingA) * kRowW + (kHc - 1) + L2 + s3 : b0;
+        constexpr int dd = kDc - kHc + 1;
+        const int32_t a0 = b0[0], a1 = b0[1], a2 = b0[2], a3 = b0[dd], a4 = b0[dd + 1];
+        const int32_t c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
+        const int32_t e0 = b2[0], e1 = b2[1], e2 = b2[2], e3 = b2[dd], e4 = b2[dd + 1];
+        const int32_t g0 = b3[0], g1 = b3[1], g2 = b3[2], g3 = b3[dd], g4 = b3[dd + 1];
+        pred_fold<SLOTS>(A, 0, a0, a1, a2, a3, a4);
+        if (np > 1) pred_fold<SLOTS>(A, 1, c0, c1, c2, c3, c4);
+        if (np > 2) pred_fold<SLOTS>(A, 2, e0, e1, e2, e3, e4);
+        if (np > 3) pred_fold<SLOTS>(A, 3, g0, g1, g2, g3, g4);
+    } else {
+        int32_t hA, hB, hC, dB, dC;
+        pred_cells(ring + (p0 % kRingA) * kRowW, s0, lane, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, 0, hA, hB, hC, dB, dC);
+        if (np > 1) {
+            pred_cells(ring + (p1 % kRingA) * kRowW, s1, lane, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 1, hA, hB, hC, dB, dC);
+        }
+        if (np > 2) {
+            pred_cells(ring + (p2 % kRingA) * kRowW, s2, lane, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 2, hA, hB, hC, dB, dC);
+        }
+        if (np > 3) {
+            pred_cells(ring + (p3 % kRingA) * kRowW, s3, lane, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 3, hA, hB, hC, dB, dC);
+        }
+    }
+}
+
+// the predecessor terms of a row with exactly NP (1 or 2) predecessors, all
+// within the ring; reads through the padded band when every shift is in
+// [-3, 4], else bounds-checked per cell
+template <int NP, bool SLOTS>
+__device__ __forceinline__ void pred_terms_n(const int32_t *ring, int32_t off, uint32_t p0, uint32_t p1, int32_t o0,
+                                             int32_t o1, int lane, PredAcc &A)
+{
+    const int32_t s0 = off - o0, s1 = off - o1;
+    const bool inr = (uint32_t)(s0 + 3) <= 7u && (NP < 2 || (uint32_t)(s1 + 3) <= 7u);
+    constexpr int dd = kDc - kHc + 1;
+    if (__builtin_expect(inr, 1)) {
+        const int L2 = 2 * lane;
+        const int32_t *b0 = ring + (p0 % kRingA) * kRowW + (kHc - 1) + L2 + s0;
+        const int32_t *b1 = ring + (p1 % kRingA) * kRowW + (kHc - 1) + L2 + s1;
+        const int32_t a0 = b0[0], a1 = b0[1], a2 = b0[2], a3 = b0[dd], a4 = b0[dd + 1];
+        int32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+        if (NP > 1) c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
+        pred_fold<SLOTS>(A, 0, a0, a1, a2, a3, a4);
+        if (NP > 1) pred_fold<SLOTS>(A, 1, c0, c1, c2, c3, c4);
+    } else {
+        int32_t hA, hB, hC, dB, dC;
+        pred_cells(ring + (p0 % kRingA) * kRowW, s0, lane, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, 0, hA, hB, hC, dB, dC);
+        if (NP > 1) {
+            pred_cells(ring + (p1 % kRingA) * kRowW, s1, lane, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 1, hA, hB, hC, dB, dC);
+        }
+    }
+}
+
+// Spill records of the two-wave DP (rows with a successor > kRing rows
+// ahead): words [0, 128) H, [128, 256) D, 256 band offset, 257 row-max key.
+constexpr uint32_t kSpillRec = kW * 8 + 16;
+
+__device__ __forceinline__ void far_meta(const Z &z, uint32_t r, uint32_t p, int32_t vOff, int32_t vKey, int32_t &o,
+                                         int32_t &k, const int32_t *&rec)
+{
+    if (r - p <= (uint32_t)kRing) {
+        o = __builtin_amdgcn_readlane(vOff, (int)(p & 63u));
+        k = __builtin_amdgcn_readlane(vKey, (int)(p & 63u));
+        rec = nullptr;
+    } else {
+        const uint32_t sl = uni(__builtin_nontemporal_load(P<uint32_t>(z, z.L.sslot) + p));
+        rec = reinterpret_cast<const int32_t *>(z.ws + z.L.spill + (size_t)sl * kSpillRec);
+        o = uni(__builtin_nontemporal_load(rec + 256));
+        k = uni(__builtin_nontemporal_load(rec + 257));
+    }
+}
+
+__device__ __forceinline__ void far_cells(const Z &z, uint32_t p, const int32_t *rec, int32_t sh, int lane,
+                                          int32_t &hA, int32_t &hB, int32_t &hC, int32_t &dB, int32_t &dC)
+{
+    if (!rec) {
+        pred_cells(z.lds + kLdsRing + (p % kRingA) * kRowW, sh, lane, hA, hB, hC, dB, dC);
+        return;
+    }
+    const int32_t i = 2 * lane + sh;
+    auto h = [&](int32_t t) { return (uint32_t)t < (uint32_t)kW ? __builtin_nontemporal_load(rec + t) : kNegH; };
+    auto d = [&](int32_t t) { return (uint32_t)t < (uint32_t)kW ? __builtin_nontemporal_load(rec + kW + t) : kNeg; };
+    hA = h(i - 1), hB = h(i), hC = h(i + 1), dB = d(i), dC = d(i + 1);
+}
+
+// A row with a predecessor beyond the ring or more than four predecessors:
+// the full predecessor list from the graph, far rows from their spill
+// records (SPEC.md §3.1-§3.2 with every tie rule)
+template <bool SLOTS>
+__device__ __forceinline__ void far_terms(const Z &z, uint32_t r, uint32_t np, int32_t vOff, int32_t vKey, int32_t lim,
+                                       bool place, int32_t &off, PredAcc &A)
+{
+    const int lane = lane_id();
+    const uint32_t po = uni(G_poff(z, z.cur)[r]);
+    const uint32_t *pl = G_pred(z, z.cur) + po;
+    if (place) {
+        off = 0;
+        int32_t bm = INT32_MIN, barg = 0;
+        for (uint32_t s = 0; s < np; ++s) {
+            const uint32_t p = uni(pl[s]);
+            int32_t o, k;
+            const int32_t *rec;
+            far_meta(z, r, p, vOff, vKey, o, k, rec);
+            if ((k >> 7) > bm) bm = k >> 7, barg = o + 127 - (k & 127);
+        }
+        if (np) off = min(max(barg + 1 - kW / 2, 0), lim);
+    }
+    if (np == 0) {
+        pred_fold<SLOTS>(A, 0, kNegH, kNegH, kNegH, kNeg, kNeg);
+        return;
+    }
+    for (uint32_t s = 0; s < np; ++s) {
+        const uint32_t p = uni(pl[s]);
+        int32_t o, k, hA, hB, hC, dB, dC;
+        const int32_t *rec;
+        far_meta(z, r, p, vOff, vKey, o, k, rec);
+        far_cells(z, p, rec, off - o, lane, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, s, hA, hB, hC, dB, dC);
+    }
+}
+
+// the 64-row record window of a wave: superblock s + 1 is loaded during the
+// second block of superblock s and becomes current after its last block
+// (before any store of that block, so the wait covers only old accesses)
+struct RecWin {
+    RowPre cur, nxt;
+};
+
+__device__ __forceinline__ void recwin_begin(const Z &z, RecWin &W, uint32_t r0)
+{
+    if (r0 == 0) {
+        prefetch_recs(z, 0, W.nxt);
+        W.cur = W.nxt;
+    } else if ((r0 & 63u) == (uint32_t)kBlkAB) {
+        prefetch_recs(z, r0 - kBlkAB + 64, W.nxt);
+    }
+}
+
+__device__ __forceinline__ void recwin_end(RecWin &W, uint32_t r0)
+{
+    if ((r0 & 63u) == 64u - kBlkAB) W.cur = W.nxt;
+}
+
+struct AState {
+    int32_t H0, H1, D0, D1;  // row r-1, this lane's two cells
+    int32_t pOff, pArg;      // row r-1: band offset, position of its maximum
+    int32_t vOff, vKey;      // lane (q & 63): band offset / row-max key of row q
+    uint32_t qn;             // read codes at the next row's chain offset (loaded a row ahead)
+    uint32_t nspill;         // spill records written
+    RecWin W;
+};
+
+// per-lane constants of a row (t0 = 2 lane, t1 = t0 + 1)
+struct LaneK {
+    int32_t L2, L4, kc0, kc1, cI0, cI1, src0;  // src0: O + E t0
+};
+
+__device__ __forceinline__ LaneK lane_consts(int lane)
+{
+    LaneK c;
+    c.L2 = 2 * lane, c.L4 = 4 * lane;
+    c.kc0 = 127 - c.L2, c.kc1 = 126 - c.L2;
+    c.cI0 = kO + kE * c.L2, c.cI1 = kO + kE * (c.L2 + 1);
+    c.src0 = kO + kE * c.L2;
+    return c;
+}
+
+// wave 0, the rows that are not "chain, band moved by 1": chain rows moved
+// by 0 or 2 (DPP) and general rows (predecessors from the ring)
+__device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r, uint32_t info, int32_t coff,
+                                         int32_t lim, int32_t &off_o, int32_t &Mh0, int32_t &Mh1, int32_t &Dv0,
+                                         int32_t &Dv1)
+{
+    const int lane = lane_id();
+    const int li = (int)(r & 63u);
+    const uint32_t np = info >> 8;
+    const int32_t sh = coff - S.pOff;
+    const int32_t *ring = z.lds + kLdsRing;
+    PredAcc A;
+    int32_t off;
+    if (info & kInfoFar) {
+        far_terms<false>(z, r, np, S.vOff, S.vKey, lim, true, off, A);
+    } else if ((info & kInfoChain) && (uint32_t)sh <= 2u) {
+        // chain row, band moved by 0..2 (1: a spill row)
+        off = coff;
+        int32_t hA, hB, hC, dB, dC;
+        if (sh == 0) {
+            hA = wave_shr1(kNegH, S.H1), hB = S.H0, hC = S.H1, dB = S.D0, dC = S.D1;
+        } else if (sh == 1) {
+            hA = S.H0, hB = S.H1, hC = wave_shl1(kNegH, S.H0), dB = S.D1, dC = wave_shl1(kNeg, S.D0);
+        } else {
+            hA = S.H1, hB = wave_shl1(kNegH, S.H0), hC = wave_shl1(kNegH, S.H1);
+            dB = wave_shl1(kNeg, S.D0), dC = wave_shl1(kNeg, S.D1);
+        }
+        pred_fold<false>(A, 0, hA, hB, hC, dB, dC);
+    } else if (np == 1) {
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
+        const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
+        const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
+        off = min(max(o0 + 127 - (k0 & 127) + 1 - kW / 2, 0), lim);
+        pred_terms_n<1, false>(ring, off, p0, p0, o0, o0, lane, A);
+    } else if (np == 2) {
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
+        const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
+        const int32_t o1 = __builtin_amdgcn_readlane(S.vOff, (int)(p1 & 63u));
+        const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
+        const int32_t k1 = __builtin_amdgcn_readlane(S.vKey, (int)(p1 & 63u));
+        // band placement (SPEC.md §3.1): first predecessor with the largest row max
+        const bool second = (k1 >> 7) > (k0 >> 7);
+        const int32_t ko = second ? k1 : k0, oo = second ? o1 : o0;
+        off = min(max(oo + 127 - (ko & 127) + 1 - kW / 2, 0), lim);
+        pred_terms_n<2, false>(ring, off, p0, p1, o0, o1, lane, A);
+    } else {
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
+        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p2, li);
+        const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p3, li);
+        const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
+        const int32_t o1 = __builtin_amdgcn_readlane(S.vOff, (int)(p1 & 63u));
+        const int32_t o2 = __builtin_amdgcn_readlane(S.vOff, (int)(p2 & 63u));
+        const int32_t o3 = __builtin_amdgcn_readlane(S.vOff, (int)(p3 & 63u));
+        const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
+        const int32_t k1 = __builtin_amdgcn_readlane(S.vKey, (int)(p1 & 63u));
+        const int32_t k2 = __builtin_amdgcn_readlane(S.vKey, (int)(p2 & 63u));
+        const int32_t k3 = __builtin_amdgcn_readlane(S.vKey, (int)(p3 & 63u));
+        off = 0;
+        if (np) {
+            int32_t bm = k0 >> 7, barg = o0 + 127 - (k0 & 127);
+            if ((k1 >> 7) > bm) bm = k1 >> 7, barg = o1 + 127 - (k1 & 127);
+            if ((k2 >> 7) > bm) bm = k2 >> 7, barg = o2 + 127 - (k2 & 127);
+            if (np > 3 && (k3 >> 7) > bm) bm = k3 >> 7, barg = o3 + 127 - (k3 & 127);
+            off = min(max(barg + 1 - kW / 2, 0), lim);
+        }
+        pred_terms<false>(ring, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
+    }
+    off_o = off, Mh0 = A.Mh0, Mh1 = A.Mh1, Dv0 = A.Dv0, Dv1 = A.Dv1;
+}
+
+// wave 0: one DP row (SPEC.md §3.1-§3.4 values)
+__device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim, const LaneK &c)
+{
+    const int lane = lane_id();
+    const int li = (int)(r & 63u);
+    const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
+    const uint32_t base = info & 3u;
+    const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
+    const uint8_t *rdl = z.rd + lane;
+    uint32_t qraw = S.qn;
+    int32_t off, Mh0, Mh1, Dv0, Dv1;
+    const bool fast = (info & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain && coff - S.pOff == 1;
+    if (__builtin_expect(fast, 1)) {
+        // the only predecessor is row r-1 and the band moved by one: its
+        // cells are in registers, shifted one lane by DPP
+        off = coff;
+        const int32_t hC = wave_shl1(kNegH, S.H0), dC = wave_shl1(kNeg, S.D0);
+        Mh0 = S.H0, Mh1 = S.H1;
+        Dv0 = max(S.H1 + (kO + kE), S.D1 + kE);
+        Dv1 = max(hC + (kO + kE), dC + kE);
+    } else {
+        dpA_cold(z, S, r, info, coff, lim, off, Mh0, Mh1, Dv0, Dv1);
+        if (off != coff) qraw = rdl[off >> 1];
+    }
+    const uint32_t qp = qraw >> ((uint32_t)(off & 1) * 4u);
+    const uint32_t q0 = qp & 3u, q1 = (qp >> 2) & 3u;
+    const int32_t srcu = c.src0 + kE * off;
+    const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
+    const int32_t M0 = max(Mh0, src0) + (q0 == base ? kMs : kXs);
+    const int32_t M1 = max(Mh1, srcu + kE) + (q1 == base ? kMs : kXs);
+    const int32_t hp0 = max(M0, Dv0), hp1 = max(M1, Dv1);
+    const int32_t X0 = hp0 + c.L4;
+    int32_t incl = max(X0, hp1 + c.L4 + 2);
+    int32_t rk = max((hp0 << 7) | c.kc0, (hp1 << 7) | c.kc1);
+    wave_incl_max2(incl, rk);
+    const int32_t Pex = wave_shr1(kNeg, incl);
+    const int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(max(Pex, X0) + c.cI1, hp1);
+    const int32_t key = __builtin_amdgcn_readlane(rk, 63);
+    // ring row, {M0, M1, Pex} for wave 1, meta window
+    int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kHc + c.L2);
+    row[0] = make_int2(nH0, nH1);
+    row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
+    int32_t *pub = z.lds + kLdsPub + (r % kPubSlots) * 192 + lane;
+    pub[0] = M0;
+    pub[64] = M1;
+    pub[128] = Pex;
+    S.vOff = writelane(S.vOff, off, li);
+    S.vKey = writelane(S.vKey, key, li);
+    if (!fast && (info & kInfoSpill)) {
+        // a successor lies beyond the ring: keep this row in HBM
+        const uint32_t sl = S.nspill++;
+        if (sl < z.d.scap) {
+            int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)sl * kSpillRec);
+            reinterpret_cast<int2 *>(rec)[lane] = make_int2(nH0, nH1);
+            reinterpret_cast<int2 *>(rec + kW)[lane] = make_int2(Dv0, Dv1);
+            if (lane == 0) rec[256] = off, rec[257] = key, P<uint32_t>(z, z.L.sslot)[r] = sl;
+        } else {
+            z.status = kErrSpill;
+        }
+        wsync();  // visible to both waves before any reader (> kRing rows later)
+    }
+    S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
+    S.pOff = off;
+    S.pArg = off + 127 - (key & 127);
+    S.qn = rdl[min(max(S.pArg + 1 - kW / 2, 0), lim) >> 1];
+}
+
+// wave 0: rows [r0, r0 + kBlkAB)
+__device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t m)
+{
+    const int lane = lane_id();
+    const int32_t lim = (int32_t)m - kW;
+    const LaneK c = lane_consts(lane);
+    recwin_begin(z, S.W, r0);
+    dpA_row(z, S, r0, lim, c);
+    if (r0 + 1 < z.R) dpA_row(z, S, r0 + 1, lim, c);
+    z.lds[kLdsOffRing + lane] = S.vOff;  // band offsets of the last 64 rows for wave 1
+    recwin_end(S.W, r0);
+}
+
+struct BState {
+    int32_t bE;       // best free-end value of this lane's cells
+    uint32_t bKey;    // its row * 2 + cell
+    uint32_t vMi;     // lane (q & 63): multi-slot ordinal of row q or kNone
+    uint32_t nmulti, mg0;  // multi rows so far / at the start of the flush group
+    RecWin W;
+    FlushBuf fa, fb;
+};
+
+// wave 1: the predecessor terms of a row that does not have exactly one
+// in-band predecessor (0 or >= 2 predecessors, or a far band shift)
+__device__ __forceinline__ void dpB_cold(const Z &z, const BState &S, uint32_t r, uint32_t info, int32_t off,
+                                         int32_t vOff, PredAcc &A)
+{
+    const int lane = lane_id();
+    const int li = (int)(r & 63u);
+    const uint32_t np = info >> 8;
+    const int32_t *ring = z.lds + kLdsRing;
+    if (info & kInfoFar) {
+        int32_t o = off;
+        // the keys of rows in the ring are wave 0's; band placement is not redone here
+        far_terms<true>(z, r, np, vOff, 0, 0, false, o, A);
+        return;
+    }
+    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
+    const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
+    const int32_t o0 = __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
+    const int32_t o1 = __builtin_amdgcn_readlane(vOff, (int)(p1 & 63u));
+    if (np == 2) {
+        pred_terms_n<2, true>(ring, off, p0, p1, o0, o1, lane, A);
+    } else if (np == 1) {
+        pred_terms_n<1, true>(ring, off, p0, p0, o0, o0, lane, A);
+    } else {
+        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p2, li);
+        const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p3, li);
+        const int32_t o2 = __builtin_amdgcn_readlane(vOff, (int)(p2 & 63u));
+        const int32_t o3 = __builtin_amdgcn_readlane(vOff, (int)(p3 & 63u));
+        pred_terms<true>(ring, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
+    }
+}
+
+// wave 1: the decision bits of one row (wave 0 wrote its ring row and {M, Pex})
+__device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m, int32_t lim, int32_t vOff,
+                                        const LaneK &c)
+{
+    const int lane = lane_id();
+    const int li = (int)(r & 63u);
+    const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
+    const uint32_t np = info >> 8;
+    const int32_t off = __builtin_amdgcn_readlane(vOff, li);
+    const int32_t *pub = z.lds + kLdsPub + (r % kPubSlots) * 192 + lane;
+    const int32_t M0 = pub[0], M1 = pub[64], Pex = pub[128];
+    const int2 Dv = reinterpret_cast<const int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kDc + c.L2)[0];
+    PredAcc A;
+    A.Dv0 = Dv.x, A.Dv1 = Dv.y;
+    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
+    const int32_t sh = off - __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
+    bool multi = false;
+    if (__builtin_expect(np == 1 && (uint32_t)(sh + 3) <= 7u && !(info & kInfoFar), 1)) {
+        // one predecessor in the padded band: its H at t-1, t, t+1; D-ext is
+        // D > H + O + E (D = max(H + O + E, D' + E))
+        const int32_t *b = z.lds + kLdsRing + (p0 % kRingA) * kRowW + (kHc - 1) + c.L2 + sh;
+        const int32_t hA = b[0], hB = b[1], hC = b[2];
+        A.Mh0 = hA, A.Mh1 = hB;
+        A.ms0 = A.ms1 = A.ds0 = A.ds1 = 0;
+        A.dx0 = A.Dv0 > hB + (kO + kE) ? 4u : 0u;
+        A.dx1 = A.Dv1 > hC + (kO + kE) ? 4u : 0u;
+    } else {
+        dpB_cold(z, S, r, info, off, vOff, A);
+        multi = np > 1;
+    }
+    const int32_t srcu = c.src0 + kE * off;
+    const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
+    const bool mp0 = A.Mh0 >= src0, mp1 = A.Mh1 >= srcu + kE;
+    const bool d0 = A.Dv0 > M0, d1 = A.Dv1 > M1;
+    const int32_t hp0 = max(M0, A.Dv0), hp1 = max(M1, A.Dv1);
+    // insertions (SPEC.md §3.4) from wave 0's exclusive prefix max
+    const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
+    const int32_t X1L = wave_shr1(INT32_MAX, X1);
+    const int32_t ex1 = max(Pex, X0);
+    const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
+    const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
+    const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
+    const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
+    const uint32_t code = (hc0 | A.dx0 | iext0) | ((hc1 | A.dx1 | iext1) << 4);
+    // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
+    // H' at j = m - 1 (lane 63, cell 1 when off == lim)
+    const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
+    const int32_t e0 = X0 + eb;
+    const int32_t e1 = X1 + eb + ((off == lim && lane == 63) ? 3 : 0);
+    if (e0 > S.bE) S.bE = e0, S.bKey = r * 2;
+    if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1;
+    uint32_t mi = kNone;
+    if (multi) {
+        // slots of a multi-predecessor row (SPEC.md §4); an MSRC cell's M slot is 0
+        const uint32_t s_m0 = mp0 ? A.ms0 : 0u, s_m1 = mp1 ? A.ms1 : 0u;
+        reinterpret_cast<uint32_t *>(z.lds + kLdsStSlots)[(S.nmulti - S.mg0) * 64 + lane] =
+            s_m0 | (s_m1 << 8) | (A.ds0 << 16) | (A.ds1 << 24);
+        mi = S.nmulti++;
+    }
+    reinterpret_cast<uint8_t *>(z.lds + kLdsStCodes)[(r & 15u) * 64 + lane] = (uint8_t)code;
+    S.vMi = (uint32_t)writelane((int)S.vMi, (int)mi, li);
+}
+
+// wave 1: rows [r0, r0 + kBlkAB), then the 16-row group's flush
+__device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t m, FlushBuf &f)
+{
+    const int lane = lane_id();
+    const uint32_t R = z.R;
+    const int32_t lim = (int32_t)m - kW;
+    const LaneK c = lane_consts(lane);
+    recwin_begin(z, S.W, r0);
+    const int32_t vOff = z.lds[kLdsOffRing + lane];
+    dpB_row(z, S, r0, m, lim, vOff, c);
+    if (r0 + 1 < R) dpB_row(z, S, r0 + 1, m, lim, vOff, c);
+    const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
+    recwin_end(S.W, r0);
+    if ((r0 & 15u) == 16u - kBlkAB || rend == R) {
+        if (S.nmulti > z.d.mcap) z.status = kErrMulti;
+        pin(f);
+        const uint32_t g0 = r0 & ~15u;
+        const uint32_t nm = z.status ? 0u : S.nmulti - S.mg0;
+        const uint32_t nrow = z.status ? 0u : rend - g0;
+        f.code = reinterpret_cast<const uint4 *>(z.lds + kLdsStCodes)[lane];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            f.slot[k] = reinterpret_cast<const uint4 *>(z.lds + kLdsStSlots)[(uint32_t)lane + 64u * k];
+        f.meta = make_uint2((uint32_t)vOff, S.vMi);
+        const auto rc = brsrc(z.ws + z.L.codes + (size_t)g0 * 64, nrow * 64);
+        const auto rm = brsrc(reinterpret_cast<uint2 *>(z.ws + z.L.rmeta) + g0, nrow * 8);
+        const auto rs = brsrc(z.ws + z.L.slots + (size_t)S.mg0 * 256, nm * 256);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{f.code.x, f.code.y, f.code.z, f.code.w}, rc, lane * 16, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(v2u{f.meta.x, f.meta.y}, rm, (uint32_t)(lane - (int)(g0 & 63u)) * 8u,
+                                              0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(v4u{f.slot[k].x, f.slot[k].y, f.slot[k].z, f.slot[k].w}, rs,
+                                                   ((uint32_t)lane + 64u * k) * 16u, 0, 0);
+        S.mg0 = S.nmulti;
+    }
+}
+
+__device__ __forceinline__ uint32_t dp_nblk(uint32_t R) { return (R + kBlkAB - 1) / kBlkAB; }
+
+// wave 0's side of a two-wave DP (wave 1 is in dp_helper)
+__device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
+{
+    const int lane = lane_id();
+    for (int i = lane; i < kRingA * 16; i += 64) {
+        const int k = i & 15;
+        const int w = k < 4 ? k : k < 8 ? kHc + kW + (k - 4) : k < 12 ? kDc - 4 + (k - 8) : kDc + kW + (k - 12);
+        z.lds[kLdsRing + (i >> 4) * kRowW + w] = k < 8 ? kNegH : kNeg;
+    }
+    volatile DpJob *job = dp_job(z);
+    if (lane == 0) job->kind = kJobDp, job->m = m, job->R = z.R, job->cur = (uint32_t)z.cur;
+    __syncthreads();  // J: job posted
+    AState S;
+    S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
+    S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0;
+    S.qn = z.rd[lane];
+    S.nspill = 0;
+    S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
+    S.W.nxt = S.W.cur;
+    const uint32_t nblk = dp_nblk(z.R);
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
+    for (uint32_t b = 0; b <= nblk; ++b) {
+        if (b < nblk) dpA_block(z, S, b * kBlkAB, m);
+        DP_STAMP(kPfAbusy);
+        lds_barrier();
+        DP_STAMP(kPfAwait);
+    }
+    er_out = job->er;
+    ej_out = job->ej;
+    if (job->status && !z.status) z.status = job->status;
+    z.cells += (unsigned long long)z.R * (uint32_t)kW;
+}
+
+// wave 1's side of one DP
+__device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m)
+{
+    const int lane = lane_id();
+    BState S;
+    S.bE = INT32_MIN, S.bKey = 0, S.vMi = kNone, S.nmulti = 0, S.mg0 = 0;
+    S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
+    S.W.nxt = S.W.cur;
+    S.fa.code = S.fb.code = make_uint4(0, 0, 0, 0);
+    S.fa.meta = S.fb.meta = make_uint2(0, 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) S.fa.slot[c] = S.fb.slot[c] = make_uint4(0, 0, 0, 0);
+    const uint32_t nblk = dp_nblk(z.R);
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
+    for (uint32_t b = 0; b <= nblk; ++b) {
+        if (b >= 1 && !z.status) {
+            const uint32_t bb = b - 1;
+            if ((bb * kBlkAB >> 4) & 1u) dpB_block(z, S, bb * kBlkAB, m, S.fb);
+            else dpB_block(z, S, bb * kBlkAB, m, S.fa);
+        }
+        if (b == nblk) {
+            // results: lexicographic (max score, min row, min j) over the lanes
+            pin(S.fa);
+            pin(S.fb);
+            const int32_t best = wave_max(S.bE);
+            const uint32_t rsel = S.bE == best ? S.bKey >> 1 : 0x7FFFFFFFu;
+            const int32_t rmin = wave_min((int32_t)rsel);
+            const bool mine = S.bE == best && (S.bKey >> 1) == (uint32_t)rmin;
+            const uint32_t tsel = mine ? 2u * (uint32_t)lane + (S.bKey & 1u) : 0x7FFFFFFFu;
+            const int32_t tmin = wave_min((int32_t)tsel);
+            wsync();
+            uint32_t ej = 0;
+            if (!z.status) ej = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin].x + (uint32_t)tmin;
+            volatile DpJob *job = dp_job(z);
+            if (lane == 0) job->er = (uint32_t)rmin, job->ej = ej, job->status = z.status, job->nmulti = S.nmulti;
+        }
+        DP_STAMP(kPfBbusy);
+        lds_barrier();
+        DP_STAMP(kPfBwait);
+    }
+}
+
+// wave 1: serve DP jobs until wave 0 posts kJobExit
+__device__ __forceinline__ void dp_helper(Z &z)
+{
+    for (;;) {
+        __syncthreads();  // J: job posted
+        volatile DpJob *job = dp_job(z);
+        const int32_t kind = job->kind;
+        if (kind == kJobExit) break;
+        z.R = job->R;
+        z.cur = (int)job->cur;
+        z.status = kOk;
+        dp_wave_b(z, job->m);
+    }
+}
+
+__device__ __forceinline__ void dp_helper_exit(Z &z)
+{
+    if (lane_id() == 0) dp_job(z)->kind = kJobExit;
+    __syncthreads();
+    // wave 1 hands over its diagnostic counters
+    __syncthreads();
+    const volatile unsigned long long *pf1 = reinterpret_cast<const volatile unsigned long long *>(z.lds + kLdsPub);
+    z.pf[kPfBbusy] += pf1[0];
+    z.pf[kPfBwait] += pf1[1];
+}
+
 __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
 {
+    if (m >= (uint32_t)kW && m < (1u << 22)) {
+        z.pf[kPfTwRows] += z.R;
+        dp_two_wave(z, m, er_out, ej_out);
+        return;
+    }
+    z.pf[kPfSwRows] += z.R;
     DpState S;
     S.bE = INT32_MIN, S.bKey = 0, S.nmulti = 0, S.nspill = 0;
     S.pH0 = S.pH1 = S.pD0 = S.pD1 = kNeg, S.pOff = 0, S.pRm = 0, S.pRarg = 0;
@@ -640,14 +1396,14 @@ __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uin
     const uint32_t rsel = S.bE == best ? S.bKey >> 1 : 0x7FFFFFFFu;
     const int32_t rmin = wave_min((int32_t)rsel);
     const bool mine = S.bE == best && (S.bKey >> 1) == (uint32_t)rmin;
-    const uint32_t tsel = mine ? 2u * (uint32_t)threadIdx.x + (S.bKey & 1u) : 0x7FFFFFFFu;
+    const uint32_t tsel = mine ? 2u * (uint32_t)lane_id() + (S.bKey & 1u) : 0x7FFFFFFFu;
     const int32_t tmin = wave_min((int32_t)tsel);
     er_out = (uint32_t)rmin;
-    __syncthreads();
+    wsync();
     const uint2 em = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin];  // flushed band offset of the end row
     ej_out = em.x + (uint32_t)tmin;
     z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
-    __syncthreads();
+    wsync();
 }
 
 // ----------------------------------------------------------------------------
@@ -685,7 +1441,7 @@ constexpr uint64_t kTbNext[3] = {tb_table(0, false), tb_table(1, false), tb_tabl
 
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = lane_id();
     uint32_t *ev = P<uint32_t>(z, z.L.ev);
     for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
     const uint32_t *poff = G_poff(z, z.cur);
@@ -736,7 +1492,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             *reinterpret_cast<uint4 *>(tbc + o) = *reinterpret_cast<const uint4 *>(codes + (size_t)blo * 64 + o);
         for (uint32_t o = lane * 16; o < nms * 256; o += 1024)
             *reinterpret_cast<uint4 *>(tbs + o) = *reinterpret_cast<const uint4 *>(slots + (size_t)mi_lo * 256 + o);
-        __syncthreads();
+        wsync();
         DP_STAMP(kPfSpare0);
         // The wave walks the block.  In state H a probe first follows the
         // diagonal run in one go: lane i checks that cell (r - i, j - i) is
@@ -824,9 +1580,9 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         lead_j = (uint32_t)__builtin_amdgcn_readfirstlane((int)lead_j);
         far_pred = (uint32_t)__builtin_amdgcn_readfirstlane((int)far_pred);
         if (far_pred != kNone) r = uni(pred[far_pred]);  // the step's predecessor, slot >= 4
-        __syncthreads();
+        wsync();
         for (uint32_t i = lane; i < nev; i += 64) ev[jhi - (int32_t)i] = evs[i];
-        __syncthreads();
+        wsync();
         DP_STAMP(kPfFlush);
     }
     if (err) {
@@ -834,7 +1590,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         return;
     }
     for (uint32_t jj = lane; jj < lead_j; jj += 64) ev[jj] = (EV_LEAD << 30) | lead_row;
-    __syncthreads();
+    wsync();
 }
 
 // ----------------------------------------------------------------------------
@@ -855,7 +1611,7 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
 
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
 {
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = lane_id();
     const uint32_t R = z.R, nw = z.d.nw;
     const int a = z.cur, b = a ^ 1;
     const uint8_t *nb = G_nb(z, a);
@@ -935,12 +1691,12 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
     }
     // M2: shift[x] = #new items with point <= x
     for (uint32_t x = lane; x <= R; x += 64) cnt[x] = 0, fixf[x] = 0;
-    __syncthreads();
+    wsync();
     for (uint32_t i = lane; i < K; i += 64) {
         atomicAdd(&cnt[ipt[i]], 1u);
         if (ifix[i] != kNone) fixf[ifix[i]] = 1;
     }
-    __syncthreads();
+    wsync();
     {
         uint32_t carry = 0;
         for (uint32_t x0 = 0; x0 <= R; x0 += 64) {
@@ -951,14 +1707,14 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
             carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         }
     }
-    __syncthreads();
+    wsync();
     const uint32_t *shift = cnt;
     auto newidx = [&](uint32_t t) -> uint32_t {
         return (t & kNewBit) ? ipt[t & ~kNewBit] + (t & ~kNewBit) : t + shift[t];
     };
     // M3: at most one new in-edge per target of this read (dedup vs existing)
     for (uint32_t x = lane; x < R2; x += 64) addp[x] = kNone;
-    __syncthreads();
+    wsync();
     for (uint32_t j = 1 + lane; j < m; j += 64) {
         const uint32_t s = tgt[j - 1], d = tgt[j];
         bool dup = false;
@@ -972,7 +1728,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         }
         if (!dup) addp[newidx(d)] = newidx(s);
     }
-    __syncthreads();
+    wsync();
     // M4: rows of the new graph
     for (uint32_t x = lane; x < R; x += 64) {
         const uint32_t n = x + shift[x];
@@ -988,7 +1744,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = 0;
         cntn[n] = addp[n] != kNone ? 1u : 0u;
     }
-    __syncthreads();
+    wsync();
     for (uint32_t j = lane; j < m; j += 64) {
         const uint32_t n = newidx(tgt[j]);
         mem2[(size_t)n * nw + (k >> 6)] |= 1ull << (k & 63u);
@@ -1010,29 +1766,49 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         }
         z.E = E2;
     }
-    __syncthreads();
+    wsync();
+    // predecessor lists of the new graph, and each row's DP record
+    // {base | chain << 3 | np << 8, p0, p1, p2} + p3 (dp_fast's prefetch)
+    uint4 *rrec = P<uint4>(z, z.L.rrec);
+    uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
     uint32_t slow = 0;
     for (uint32_t x = lane; x < R; x += 64) {
         const uint32_t n = x + shift[x];
         uint32_t o = poff2[n];
-        const uint32_t e1 = poff[x + 1];
-        slow |= (e1 - poff[x] + (addp[n] != kNone ? 1u : 0u)) > 4u;
-        for (uint32_t e = poff[x]; e < e1; ++e) {
+        const uint32_t e0 = poff[x], e1 = poff[x + 1];
+        const uint32_t ad = addp[n];
+        const uint32_t np = e1 - e0 + (ad != kNone ? 1u : 0u);
+        slow |= np > 4u;
+        uint32_t ps[4] = {0, 0, 0, 0}, s = 0;
+        for (uint32_t e = e0; e < e1; ++e, ++s) {
             const uint32_t p = pred[e] + shift[pred[e]];
             pred2[o++] = p;
+            if (s < 4) ps[s] = p;
             if (n - p > (uint32_t)kRing) spf[p] = 1, slow = 1;
         }
-        if (addp[n] != kNone) {
-            pred2[o] = addp[n];
-            if (n - addp[n] > (uint32_t)kRing) spf[addp[n]] = 1, slow = 1;
+        if (ad != kNone) {
+            pred2[o] = ad;
+            if (s < 4) ps[s] = ad;
+            if (n - ad > (uint32_t)kRing) spf[ad] = 1, slow = 1;
         }
+        const uint32_t chain = (np == 1 && ps[0] + 1 == n) ? kInfoChain : 0u;
+        uint32_t far = np > 4u ? kInfoFar : 0u;
+        for (uint32_t e = e0; e < e1; ++e) far |= n - (pred[e] + shift[pred[e]]) > (uint32_t)kRing ? kInfoFar : 0u;
+        if (ad != kNone && n - ad > (uint32_t)kRing) far = kInfoFar;
+        rrec[n] = make_uint4((nb[x] & 3u) | chain | far | (np << 8), ps[0], ps[1], ps[2]);
+        rp3[n] = ps[3];
     }
     for (uint32_t i = lane; i < K; i += 64) {
         const uint32_t n = ipt[i] + i;
-        if (addp[n] != kNone) {
-            pred2[poff2[n]] = addp[n];
-            if (n - addp[n] > (uint32_t)kRing) spf[addp[n]] = 1, slow = 1;
+        const uint32_t ad = addp[n];
+        uint32_t info = (uint32_t)iinf[i] & 3u;
+        if (ad != kNone) {
+            pred2[poff2[n]] = ad;
+            if (n - ad > (uint32_t)kRing) spf[ad] = 1, slow = 1;
+            info |= (1u << 8) | (ad + 1 == n ? kInfoChain : 0u) | (n - ad > (uint32_t)kRing ? kInfoFar : 0u);
         }
+        rrec[n] = make_uint4(info, ad != kNone ? ad : 0u, 0u, 0u);
+        rp3[n] = 0;
     }
     z.slow = ballot(slow != 0) != 0;
     // M5: first/last rows of the reads
@@ -1048,7 +1824,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
     }
     z.R = R2;
     z.cur = b;
-    __syncthreads();
+    wsync();
 }
 
 // ----------------------------------------------------------------------------
@@ -1056,7 +1832,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
 {
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = lane_id();
     const uint32_t R = z.R, nw = z.d.nw;
     const uint8_t *nb = G_nb(z, z.cur);
     const uint64_t *mem = G_mem(z, z.cur);
@@ -1078,12 +1854,12 @@ __device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
     }
     const uint32_t ncols = carry;
     if (lane == 0) colrow[ncols] = R;
-    __syncthreads();
+    wsync();
     for (uint32_t k = lane; k < n; k += 64) {
         rfc[k] = rfirst[k] != kNone ? colof[rfirst[k]] : kNone;
         rlc[k] = rfirst[k] != kNone ? colof[rlast[k]] : 0u;
     }
-    __syncthreads();
+    wsync();
     for (uint32_t c = lane; c < ncols; c += 64) {
         const uint32_t a = colrow[c], e = colrow[c + 1];
         uint32_t cnt[4] = {0, 0, 0, 0}, tot = 0, cov = 0;
@@ -1105,7 +1881,7 @@ __device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
             if ((nb[u] & 3u) == cb) crow = u;
         for (uint32_t w = 0; w < nw; ++w) cmask[(size_t)c * nw + w] = crow != kNone ? mem[(size_t)crow * nw + w] : 0ull;
     }
-    __syncthreads();
+    wsync();
     return ncols;
 }
 
@@ -1119,11 +1895,11 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
     z.R = 0;
     z.E = 0;
     z.cur = 0;
-    if (threadIdx.x == 0) G_poff(z, 0)[0] = 0;
+    if (lane_id() == 0) G_poff(z, 0)[0] = 0;
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t m = uni(rdlen[k]);
-        if (threadIdx.x == 0) rfirst[k] = rlast[k] = kNone;
-        __syncthreads();
+        if (lane_id() == 0) rfirst[k] = rlast[k] = kNone;
+        wsync();
         if (m == 0) continue;
         if (m > z.rdcap || m > z.d.lcap) {
             z.status = kErrReadLen;
@@ -1187,7 +1963,7 @@ __device__ __forceinline__ uint32_t find_breakpoint(const Z &z, uint32_t ncols, 
     const uint32_t window = 10;
     if (ncols <= window) return 0;  // SPEC.md §7 (main.c:580 would underflow)
     for (int32_t top = (int32_t)(ncols - window); top >= 1; top -= 64) {
-        const int32_t cand = top - (int32_t)threadIdx.x;
+        const int32_t cand = top - (int32_t)lane_id();
         const bool ok = cand >= 1 && bp_ok(z, (uint32_t)cand, nseq, colrate);
         const uint64_t bal = ballot(ok);
         if (bal) return (uint32_t)(top - (int32_t)__builtin_ctzll(bal));
@@ -1198,7 +1974,7 @@ __device__ __forceinline__ uint32_t find_breakpoint(const Z &z, uint32_t ncols, 
 // emit the consensus of columns [0, i) (main.c:622-638); advance pos if flag
 __device__ __forceinline__ void emit(Z &z, uint32_t i, uint32_t ncols, uint32_t n, bool flag, uint8_t *out, uint32_t &ol)
 {
-    const uint32_t lane = threadIdx.x, nw = z.d.nw;
+    const uint32_t lane = lane_id(), nw = z.d.nw;
     const uint8_t *cons = P<uint8_t>(z, z.L.cons);
     if (flag) {
         const uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
@@ -1227,37 +2003,37 @@ __device__ __forceinline__ void emit(Z &z, uint32_t i, uint32_t ncols, uint32_t 
         ol += (uint32_t)__builtin_popcountll(bal);
     }
     if (ol > z.d.outcap) z.status = kErrOut;
-    __syncthreads();
+    wsync();
 }
 
 // tidy_msa_bspoa (main.c:572): column-major MSA with mrow = n + 4
 __device__ __forceinline__ void write_msa(Z &z, uint32_t ncols, uint32_t n, uint8_t *msa)
 {
-    const uint32_t lane = threadIdx.x, nw = z.d.nw, mrow = n + 4;
+    const uint32_t lane = lane_id(), nw = z.d.nw, mrow = n + 4;
     const uint8_t *nb = G_nb(z, z.cur);
     const uint64_t *mem = G_mem(z, z.cur);
     const uint32_t *colof = P<uint32_t>(z, z.L.colof);
     const uint8_t *cons = P<uint8_t>(z, z.L.cons);
     const uint64_t tot = (uint64_t)ncols * mrow;
     for (uint64_t x = lane; x < tot; x += 64) msa[x] = 4;
-    __syncthreads();
+    wsync();
     for (uint32_t r = lane; r < z.R; r += 64) {
         uint8_t *cp = msa + (size_t)colof[r] * mrow;
         for (uint32_t k = 0; k < n; ++k)
             if ((mem[(size_t)r * nw + (k >> 6)] >> (k & 63u)) & 1ull) cp[k + 1] = nb[r] & 3u;
     }
     for (uint32_t c = lane; c < ncols; c += 64) msa[(size_t)c * mrow + n + 1] = cons[c];
-    __syncthreads();
+    wsync();
 }
 
-__global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
+__global__ void __launch_bounds__(128, 2) ccsx_zmw_kernel(KArgs a)
 {
     extern __shared__ int32_t smem[];
     if (blockIdx.x >= a.nzmw) return;
     // longest-processing-time-first: the host orders the batch by cost so the
     // largest ZMWs start first and the tail of the launch is short ones
     const uint32_t zi = a.order[blockIdx.x];
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = lane_id();
     Z z;
     z.d = a.desc[zi];
     zlayout(z.L, z.d);
@@ -1265,14 +2041,21 @@ __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
     z.seq = a.seq + z.d.seq_off;
     z.lds = smem;
     z.meta = smem + kLdsMeta;
-    z.rd = reinterpret_cast<uint32_t *>(smem + kLdsFixed);
-    z.pos = z.rd + a.lds_read_words;
-    z.rdcap = a.lds_read_words * 16;
+    z.rd = reinterpret_cast<uint8_t *>(smem + kLdsFixed);
+    z.pos = reinterpret_cast<uint32_t *>(smem + kLdsFixed) + a.lds_read_words;
+    z.rdcap = (a.lds_read_words - 2) * 8;
     z.status = kOk;
     z.cells = 0;
     z.slow = 0;
 #pragma unroll
     for (int i = 0; i < kProfSlots; ++i) z.pf[i] = 0;
+    if (threadIdx.x >= 64) {
+        dp_helper(z);  // wave 1: the second half of every two-wave DP
+        volatile unsigned long long *pf1 = reinterpret_cast<volatile unsigned long long *>(z.lds + kLdsPub);
+        if (lane == 0) pf1[0] = z.pf[kPfBbusy], pf1[1] = z.pf[kPfBwait];
+        __syncthreads();
+        return;
+    }
     const unsigned long long t_start = stamp();
     const uint32_t n = z.d.n;
     const uint32_t *soff = a.soff + z.d.seg0, *slen = a.slen + z.d.seg0;
@@ -1283,7 +2066,7 @@ __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
     if (a.mode != kShred) {
         // ccs_for (main.c:486-502) / single bspoa call: push every segment whole
         for (uint32_t k = lane; k < n; k += 64) rdoff[k] = soff[k], rdlen[k] = slen[k];
-        __syncthreads();
+        wsync();
         const uint32_t ncols = run_poa(z, n, z.seq);
         if (!z.status) {
             emit(z, ncols, ncols, n, false, out, ol);
@@ -1300,7 +2083,7 @@ __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
         const uint32_t addlen = 2000, minlen = 1000, initlen = 2000;
         const uint32_t colrate = n < 10 ? 60u : 80u;
         for (uint32_t k = lane; k < n; k += 64) z.pos[k] = 0;
-        __syncthreads();
+        wsync();
         bool flag = true;
         while (flag && !z.status) {
             uint32_t i = 0, ncols = 0;
@@ -1313,7 +2096,7 @@ __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
                     rdoff[k] = soff[k] + z.pos[k];
                     rdlen[k] = fin ? slen[k] - z.pos[k] : ws;
                 }
-                __syncthreads();
+                wsync();
                 ncols = run_poa(z, n, z.seq);
                 if (z.status) break;
                 if (!flag) {
@@ -1331,6 +2114,7 @@ __global__ void __launch_bounds__(64) ccsx_zmw_kernel(KArgs a)
             z.pf[kPfShred] += stamp() - te0;
         }
     }
+    dp_helper_exit(z);
     if (lane == 0) {
         a.out_len[zi] = ol;
         a.status[zi] = z.status;
@@ -1352,6 +2136,6 @@ extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, 
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(64), lds_bytes, s, *a);
+    hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(128), lds_bytes, s, *a);
     return hipGetLastError();
 }

@@ -19,11 +19,15 @@ namespace ccsx {
 
 constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
 constexpr int kRing = 16;      // DP rows kept in LDS per wave
+constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H and D, each [4 pad | 128 | 4 pad]
+constexpr int kRingA = 20;     // its ring rows: kRing predecessor rows + 2 blocks of wave 1's lag
+constexpr int kPubSlots = 4;   // rows of {M0, M1, insertion prefix} handed from wave 0 to wave 1
 constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 // fixed LDS words per wave: DP ring + ring meta + flush staging (codes, meta,
 // slots); the packed read and the shredding cursors follow (ccsx_kernel.hip)
-constexpr int kLdsFixedWords = kRing * 256 + kRing * 4 + 16 * 16 + 16 * 2 + 16 * 64;
+constexpr int kLdsFixedWords =
+    kRingA * kRowW + kRing * 4 + 16 * 16 + 16 * 2 + 16 * 64 + kPubSlots * 192 + 64 + 16;
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
 enum Status : int32_t {
@@ -54,7 +58,7 @@ struct ZmwDesc {
 
 struct ZLayout {
     uint64_t nb0, mem0, poff0, pred0, nb1, mem1, poff1, pred1;
-    uint64_t rmeta, spf, sslot, codes, slots, spill;
+    uint64_t rmeta, spf, sslot, codes, slots, spill, rrec, rp3;
     uint64_t ev, tgt, ipt, iinf, ifix, cnt, fixf, addp, cntn;
     uint64_t colof, cons, cmask, colrow, rdoff, rdlen, rfirst, rlast, rfc, rlc;
     uint64_t total;
@@ -84,6 +88,8 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
     L.codes = take(uint64_t(d.rcap) * 64);             // traceback codes, 4 bits/cell, 64 B/row
     L.slots = take(uint64_t(d.mcap) * 256);            // predecessor slots of multi-predecessor rows
     L.spill = take(uint64_t(d.scap) * (kW * 8 + 16));  // spilled rows: H/D + off/rmax/rarg
+    L.rrec = take(uint64_t(d.rcap) * 16);              // per row: {info, p0, p1, p2} for the DP prefetch
+    L.rp3 = take(uint64_t(d.rcap) * 4);                // per row: 4th predecessor
     L.ev = take(uint64_t(d.lcap) * 4);
     L.tgt = take(uint64_t(d.lcap) * 4);
     L.ipt = take(uint64_t(d.lcap) * 4);
@@ -158,6 +164,9 @@ struct KArgs {
 
 // phase counters written when KArgs::prof != nullptr
 enum ProfSlot { kPfTotal = 0, kPfLoad, kPfDp, kPfTrace, kPfMerge, kPfColumns, kPfShred, kPfRows,
-                kPfRowA, kPfRowB, kPfRowC, kPfRowD, kPfRowE, kPfFlush, kPfSpare0, kPfSpare1, kProfSlots };
+                kPfRowA, kPfRowB, kPfRowC, kPfRowD, kPfRowE, kPfFlush, kPfSpare0, kPfSpare1,
+                // two-wave DP (diagnostic build): wave 0 / wave 1 busy and barrier-wait
+                // cycles, rows through the two-wave and the single-wave DP
+                kPfAbusy, kPfAwait, kPfBbusy, kPfBwait, kPfTwRows, kPfSwRows, kPfSpare2, kPfSpare3, kProfSlots };
 
 }  // namespace ccsx

@@ -21,5 +21,7 @@ tot = p["total"]
 out = {"config": vars(a), "kernel_ms": ms, "gcups": cells / ms / 1e6,
        "share": {k: round(v / tot, 4) for k, v in p.items() if k not in ("total", "dp_rows")},
        "cycles_per_zmw": tot / a.n, "row_cycles": {k: round(v / max(p["dp_rows"], 1), 1) for k, v in p.items() if k.startswith("row_")}, "tb_share": {k: round(p[k] / tot, 4) for k in ("spare0", "spare1", "flush")}, "dp_cycles_per_row": p["dp"] / max(p["dp_rows"], 1),
-       "rows_per_zmw": p["dp_rows"] / a.n}
+       "rows_per_zmw": p["dp_rows"] / a.n,
+       "two_wave": {k: round(p[k] / max(p["tw_rows"], 1), 1) for k in ("a_busy", "a_wait", "b_busy", "b_wait")},
+       "tw_rows_frac": round(p["tw_rows"] / max(p["dp_rows"], 1), 4)}
 print(json.dumps(out))
