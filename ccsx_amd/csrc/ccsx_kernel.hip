@@ -158,13 +158,11 @@ struct Z {
     uint8_t *ws;
     const uint8_t *seq;
     int32_t *lds;        // ring: kRing * 256 ints
-    int32_t *meta;       // kRing * 4 ints: off, rmax, rarg, tof
     uint8_t *rd;         // read as nibble pairs: byte b = pair(2b) | pair(2b+1) << 4, pair(j) = code(j) | code(j+1) << 2
     uint32_t *pos;       // shredding cursors
     uint32_t rdcap;      // bases that fit in rd
     int cur;
     uint32_t R, E;
-    uint32_t slow;  // current graph has a predecessor > kRing rows back or a row with > 4 predecessors
     int32_t status;
     unsigned long long cells;
     unsigned long long pf[kProfSlots];
@@ -180,7 +178,13 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t bytes)
 {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+    // every field through readfirstlane: a descriptor in VGPRs would make the
+    // compiler wrap each access in a waterfall loop
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(u), 0,
+                                             __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
 
 // Diagnostic build only (-DCCSX_DP_STAMPS, libccsx_amd_diag.so): shader-clock
@@ -241,78 +245,32 @@ __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
     wsync();
 }
 
-// read the two cells of lane l at band index 2l+c (c wave-uniform) from a row
-// stored in the even/odd split layout [Hev|Hod|Dev|Dod] x 64 ints
-template <int ARR>
-__device__ __forceinline__ int cell_lds(const int32_t *row, int c, int lane)
-{
-    const int i = 2 * lane + c;
-    if ((unsigned)i >= (unsigned)kW) return kNeg;
-    return row[(ARR + (i & 1)) * 64 + (i >> 1)];
-}
-
-template <int ARR>
-__device__ __forceinline__ int cell_glb(const int32_t *row, int c, int lane)
-{
-    const int i = 2 * lane + c;
-    if ((unsigned)i >= (unsigned)kW) return kNeg;
-    return __builtin_nontemporal_load(row + (ARR + (i & 1)) * 64 + (i >> 1));
-}
-
-struct PredRow {
-    int32_t off, rmax, rarg;
-};
-
-// LDS layout of one wave (int32 words)
-constexpr int kLdsRing = 0;                          // kRing rows: [Hev|Hod|Dev|Dod] x 64 (dp_block) or kRowW (dp_fast)
-constexpr int kLdsMeta = kRingA * kRowW;             // (spare) kRing x 4 words
-constexpr int kLdsStCodes = kLdsMeta + kRing * 4;    // kBlk rows x 64 B of codes
-constexpr int kBlk = 16;                             // rows per flush block
-constexpr int kLdsStMeta = kLdsStCodes + kBlk * 16;  // kBlk x {off, mi}
-constexpr int kLdsStSlots = kLdsStMeta + kBlk * 2;   // kBlk x 256 B of slots
-constexpr int kLdsPub = kLdsStSlots + kBlk * 64;     // kPubSlots x {M0, M1, Pex} x 64: wave 0 -> wave 1
-constexpr int kLdsOffRing = kLdsPub + kPubSlots * 192;  // 64: band offset of DP row q at q & 63
-constexpr int kLdsJob = kLdsOffRing + 64;             // 16: two-wave DP job / results
-constexpr int kLdsFixed = kLdsJob + 16;               // then: the read (nibble pairs), shredding cursors
-static_assert(kBlk == kRing, "the ring doubles as the spill source of a flushed block");
+// LDS layout of a workgroup (int32 words)
+constexpr int kLdsRing = 0;                              // kRingA DP rows x kRowW (traceback: 2 blocks)
+constexpr int kLdsStRec = kLdsRing + kRingA * kRowW;     // 16 rows x 256 B of cell records (wave 1)
+constexpr int kLdsPub = kLdsStRec + 16 * 64;             // kPubSlots x {M0, M1, Pex} x 64: wave 0 -> wave 1
+constexpr int kLdsOffRing = kLdsPub + kPubSlots * 192;   // 64: band offset of DP row q at q & 63
+constexpr int kLdsJob = kLdsOffRing + 64;                // 16: two-wave DP job / results
+constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
 static_assert(kLdsFixed == kLdsFixedWords, "host and device LDS layouts disagree");
 
-// meta of a spilled row (rows within the ring keep theirs in registers, DpState)
-__device__ __forceinline__ PredRow pred_meta(const Z &z, uint32_t r, uint32_t p)
-{
-    PredRow m;
-    {
-        const uint32_t sl = uni(__builtin_nontemporal_load(P<uint32_t>(z, z.L.sslot) + p));
-        const int32_t *rec = reinterpret_cast<const int32_t *>(z.ws + z.L.spill + (size_t)sl * (kW * 8 + 16));
-        m.off = uni(__builtin_nontemporal_load(rec + 256));
-        m.rmax = uni(__builtin_nontemporal_load(rec + 257));
-        m.rarg = uni(__builtin_nontemporal_load(rec + 258));
-    }
-    return m;
-}
-
-// Register set of one flush.  Two sets alternate (even/odd blocks) and each
-// is pinned live until it is rewritten two blocks later, so the global stores
-// of a flush never stall the DP on a store-data (WAR) wait.
+// Register set of one flush of wave 1.  Two sets alternate (even/odd 16-row
+// groups) and each is pinned live until it is rewritten a group later, so the
+// global stores of a flush never stall the DP on a store-data (WAR) wait.
 struct FlushBuf {
-    uint4 code;
     uint2 meta;
     uint4 slot[4];
 };
 
 __device__ __forceinline__ void pin(FlushBuf &f)
 {
-    asm volatile("" : "+v"(f.code.x), "+v"(f.code.y), "+v"(f.code.z), "+v"(f.code.w), "+v"(f.meta.x), "+v"(f.meta.y));
+    asm volatile("" : "+v"(f.meta.x), "+v"(f.meta.y));
 #pragma unroll
     for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(f.slot[i].x), "+v"(f.slot[i].y), "+v"(f.slot[i].z), "+v"(f.slot[i].w));
 }
 
-// ----------------------------------------------------------------------------
-// SPEC.md §3: banded read-vs-graph DP for one read (codes in z.rd, length m)
-// ----------------------------------------------------------------------------
-// per lane: row r0+lane's info (base | spill << 2 | chain << 3 | npred << 8;
-// chain = the only predecessor is the previous row), poff, first 4 predecessors
+// per lane: row r0+lane's info and first four predecessors
 struct RowPre {
     uint32_t info, po, p0, p1, p2, p3;
 };
@@ -321,35 +279,7 @@ struct RowPre {
 // predecessor lies > kRing rows back or there are > 4) | np << 8
 constexpr uint32_t kInfoSpill = 4u, kInfoChain = 8u, kInfoFar = 16u;
 
-struct DpState {
-    int32_t bE;
-    uint32_t bKey;                   // best end cell: row * 2 + (0: t0, 1: t1) of this lane
-    uint32_t nmulti, nspill;
-    int32_t pH0, pH1, pD0, pD1;      // row r-1, this lane's two cells (registers)
-    int32_t pOff, pRm, pRarg;        // row r-1 meta (uniform)
-    int32_t mOff, mRm, mRarg;        // meta ring: lane (r % kRing) holds row r's meta
-    RowPre cur, nxt;                 // rows of the current / next 64-row superblock (one row per lane)
-};
-
-__device__ __forceinline__ void prefetch_rows(const Z &z, uint32_t r0, RowPre &o)
-{
-    const uint32_t rr = r0 + lane_id();
-    if (rr < z.R) {
-        const uint8_t *nb = G_nb(z, z.cur);
-        const uint32_t *poff = G_poff(z, z.cur);
-        const uint32_t *pred = G_pred(z, z.cur);
-        o.po = poff[rr];
-        const uint32_t np = poff[rr + 1] - o.po;
-        o.p0 = np > 0 ? pred[o.po] : 0u;
-        o.p1 = np > 1 ? pred[o.po + 1] : 0u;
-        o.p2 = np > 2 ? pred[o.po + 2] : 0u;
-        o.p3 = np > 3 ? pred[o.po + 3] : 0u;
-        const uint32_t chain = (np == 1 && o.p0 + 1 == rr) ? kInfoChain : 0u;
-        o.info = ((uint32_t)nb[rr] & 3u) | ((uint32_t)P<uint8_t>(z, z.L.spf)[rr] << 2) | chain | (np << 8);
-    }
-}
-
-// dp_fast: one coalesced record per row, written by merge (no dependent loads)
+// the DP's row records (written by merge): coalesced, no dependent loads
 __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o)
 {
     const uint32_t n = r0 < z.R ? z.R - r0 : 0u;
@@ -358,308 +288,6 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
     const uint32_t sp = __builtin_amdgcn_raw_buffer_load_b8(brsrc(P<const uint8_t>(z, z.L.spf) + r0, n), lane_id(), 0, 0);
     o.info = q.x | (sp ? kInfoSpill : 0u), o.p0 = q.y, o.p1 = q.z, o.p2 = q.w;
     o.p3 = __builtin_amdgcn_raw_buffer_load_b32(brsrc(P<const uint32_t>(z, z.L.rp3) + r0, n * 4), lane_id() * 4, 0, 0);
-}
-
-// The cells of one row given the predecessor terms (SPEC.md §3.2-§3.5).
-// hA = max_s Hp_s(j0-1) (= Mh of t0), hB = Mh of t1, Dv0/Dv1 and their slot /
-// ext bits computed by the caller.  FULL: every cell of the band is valid.
-struct RowOut {
-    int32_t H0, H1, D0, D1, rm, rarg;
-    uint32_t code;  // two 4-bit cell codes (t0 low nibble)
-};
-
-template <bool FULL>
-__device__ __forceinline__ RowOut row_cells(const Z &z, DpState &S, uint32_t r, int32_t off, uint32_t m, uint32_t base,
-                                            int32_t Mh0, int32_t Mh1, int32_t Dv0, int32_t Dv1, uint32_t dx0,
-                                            uint32_t dx1)
-{
-    const int lane = lane_id();
-    const int32_t t0 = 2 * lane;
-    const int32_t j0 = off + t0, j1 = j0 + 1;
-    // read codes of the two cells: one nibble pair
-    const uint32_t qp = (uint32_t)z.rd[(uint32_t)j0 >> 1] >> (((uint32_t)j0 & 1u) * 4u);
-    const uint32_t q0 = qp & 3u, q1 = (qp >> 2) & 3u;
-    // M (SPEC.md §3.2)
-    int32_t src0 = kO + kE * j0;
-    if (off == 0) src0 = lane == 0 ? 0 : src0;
-    const int32_t src1 = kO + kE * j1;
-    const bool mp0 = Mh0 >= src0, mp1 = Mh1 >= src1;
-    const int32_t M0 = (mp0 ? Mh0 : src0) + (base == q0 ? kMs : kXs);
-    const int32_t M1 = (mp1 ? Mh1 : src1) + (base == q1 ? kMs : kXs);
-    uint32_t hc0 = mp0 ? HC_MPRED : HC_MSRC, hc1 = mp1 ? HC_MPRED : HC_MSRC;
-    const bool d0 = Dv0 > M0, d1 = Dv1 > M1;
-    const int32_t hp0 = d0 ? Dv0 : M0, hp1 = d1 ? Dv1 : M1;
-    hc0 = d0 ? HC_DEL : hc0;
-    hc1 = d1 ? HC_DEL : hc1;
-    // in-row insertions (SPEC.md §3.4): exclusive prefix max of X = H' - E*t.
-    // The row max of H equals the row max of H' (an insertion is always
-    // below the H' it extends from) and so does its first position, so the
-    // row-max reduction runs beside the scan instead of after it.
-    const int32_t X0 = hp0 - kE * t0, X1 = hp1 - kE * (t0 + 1);
-    int32_t hm0 = hp0, hm1 = hp1;
-    if (!FULL) {
-        if (j0 >= (int32_t)m) hm0 = kNeg;
-        if (j1 >= (int32_t)m) hm1 = kNeg;
-    }
-    int32_t incl = max(X0, X1), rmx = max(hm0, hm1);
-    wave_incl_max2(incl, rmx);
-    const int32_t Pex = wave_shr1(kNeg, incl);
-    const int32_t ex1 = max(Pex, X0);
-    const int32_t I0 = lane == 0 ? kNeg : kO + kE * t0 + Pex;
-    const int32_t I1 = kO + kE * (t0 + 1) + ex1;
-    const uint32_t iext1 = Pex > X0 ? 8u : 0u;
-    const uint32_t iext0 = (uint32_t)wave_shr1(0, ex1 > X1 ? 8 : 0);
-    const bool i0 = I0 > hp0, i1 = I1 > hp1;
-    RowOut o;
-    o.H0 = i0 ? I0 : hp0;
-    o.H1 = i1 ? I1 : hp1;
-    o.D0 = Dv0;
-    o.D1 = Dv1;
-    hc0 = i0 ? HC_INS : hc0;
-    hc1 = i1 ? HC_INS : hc1;
-    uint32_t c0 = hc0 | dx0 | iext0, c1 = hc1 | dx1 | iext1;
-    if (!FULL) {
-        if (j0 >= (int32_t)m) o.H0 = kNeg, o.D0 = kNeg, c0 = 0;
-        if (j1 >= (int32_t)m) o.H1 = kNeg, o.D1 = kNeg, c1 = 0;
-    }
-    o.code = c0 | (c1 << 4);
-    // row max / argmax for the successors' band placement
-    o.rm = __builtin_amdgcn_readlane(rmx, 63);
-    const uint64_t hit0 = ballot(hm0 == o.rm), hit1 = ballot(hm1 == o.rm);
-    const uint32_t c0i = hit0 ? 2u * (uint32_t)__builtin_ctzll(hit0) : 256u;
-    const uint32_t c1i = hit1 ? 2u * (uint32_t)__builtin_ctzll(hit1) + 1u : 256u;
-    o.rarg = off + (int32_t)(c0i < c1i ? c0i : c1i);
-    // free-end candidates (SPEC.md §3.5): e = H + 2j - 2m - 1, or H at j = m-1
-    const int32_t eb = 2 * j0 - 2 * (int32_t)m - 1;
-    int32_t e0 = o.H0 + eb, e1 = o.H1 + eb + 2;
-    if (j0 == (int32_t)m - 1) e0 = o.H0;
-    if (j1 == (int32_t)m - 1) e1 = o.H1;
-    if (!FULL) {
-        if (j0 >= (int32_t)m) e0 = INT32_MIN;
-        if (j1 >= (int32_t)m) e1 = INT32_MIN;
-    }
-    if (e0 > S.bE) S.bE = e0, S.bKey = r * 2;
-    if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1;
-    return o;
-}
-
-// one 16-row block of the DP, then its flush through register set f.
-// SLOW: some predecessor is further back than the LDS ring (spilled rows in
-// HBM) or has > 4 predecessors; otherwise the row loop never touches HBM.
-template <bool SLOW>
-__device__ __forceinline__ void dp_block(Z &z, DpState &S, uint32_t blk, uint32_t m, FlushBuf &f)
-{
-    const int lane = lane_id();
-    const uint32_t R = z.R;
-    const uint32_t r0 = blk * kBlk;
-    if (r0 >= R) return;
-    const uint32_t *pred = G_pred(z, z.cur);
-    const int32_t lim = m > (uint32_t)kW ? (int32_t)(m - kW) : 0;
-    uint8_t *st_codes = reinterpret_cast<uint8_t *>(z.lds + kLdsStCodes);
-    uint32_t *st_slots = reinterpret_cast<uint32_t *>(z.lds + kLdsStSlots);
-    int32_t *st_meta = z.lds + kLdsStMeta;
-    const uint32_t mi0 = S.nmulti;
-    if ((blk & 3u) == 0) {
-        if (blk == 0) prefetch_rows(z, 0, S.cur);
-        else S.cur = S.nxt;
-    } else if ((blk & 3u) == 1) {
-        // issue the next superblock's loads now; consumed 3 blocks later
-        prefetch_rows(z, (blk + 3) * kBlk, S.nxt);
-    }
-    const uint32_t rend = r0 + kBlk < R ? r0 + kBlk : R;
-    uint32_t spill_mask = 0;
-#ifdef CCSX_DP_STAMPS
-    unsigned long long t_prev = stamp();
-#endif
-    for (uint32_t r = r0; r < rend; ++r) {
-        DP_STAMP(kPfRowE);
-        const int li = (int)(r & 63u);
-        const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.info, li);
-        const uint32_t base = info & 3u, np = info >> 8;
-        if (np > 255u) {
-            z.status = kErrInDegree;
-            return;
-        }
-        RowOut o;
-        uint32_t mi = kNone;
-        int32_t off;
-        const int32_t chain_off = min(max(S.pRarg + 1 - kW / 2, 0), lim);
-        const int32_t sh1 = chain_off - S.pOff;
-        if ((info & kInfoChain) && (uint32_t)sh1 <= 2u && chain_off + kW <= (int32_t)m) {
-            // fast path: the only predecessor is the previous row, the band
-            // moved by 0..2 and is entirely inside the read: the predecessor's
-            // cells come from registers through DPP lane shifts
-            off = chain_off;
-            
-            int hA, hB, hC, dB, dC;
-            if (sh1 == 0) {
-                hA = wave_shr1(kNeg, S.pH1), hB = S.pH0, hC = S.pH1, dB = S.pD0, dC = S.pD1;
-            } else if (sh1 == 1) {
-                hA = S.pH0, hB = S.pH1, hC = wave_shl1(kNeg, S.pH0), dB = S.pD1, dC = wave_shl1(kNeg, S.pD0);
-            } else {
-                hA = S.pH1, hB = wave_shl1(kNeg, S.pH0), hC = wave_shl1(kNeg, S.pH1);
-                dB = wave_shl1(kNeg, S.pD0), dC = wave_shl1(kNeg, S.pD1);
-            }
-            // D = max(H+O+E, D+E) with NEG floor; ext only if it beats NEG
-            const int a0 = hB + kO + kE, b0 = dB + kE, a1 = hC + kO + kE, b1 = dC + kE;
-            const int32_t Dv0 = max(max(a0, b0), kNeg), Dv1 = max(max(a1, b1), kNeg);
-            const uint32_t dx0 = b0 > max(a0, kNeg) ? 4u : 0u, dx1 = b1 > max(a1, kNeg) ? 4u : 0u;
-            
-            o = row_cells<true>(z, S, r, off, m, base, hA, hB, Dv0, Dv1, dx0, dx1);
-            DP_STAMP(kPfRowA);  // fast (chain) rows
-#ifdef CCSX_DP_STAMPS
-            z.pf[kPfRowD] += 1;  // number of fast rows
-#endif
-        } else {
-            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p0, li);
-            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p1, li);
-            const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p2, li);
-            const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.cur.p3, li);
-            const uint32_t po = SLOW ? (uint32_t)__builtin_amdgcn_readlane((int)S.cur.po, li) : 0u;
-            auto predp = [&](uint32_t s) -> uint32_t {
-                if (s == 0) return p0;
-                if (s == 1) return p1;
-                if (s == 2) return p2;
-                if (s == 3 || !SLOW) return p3;
-                return uni(pred[po + s]);
-            };
-            // meta of a predecessor: from the register meta ring (rows within
-            // kRing) or, in SLOW mode, a spilled row's record
-            auto meta = [&](uint32_t p) -> PredRow {
-                if (!SLOW || r - p <= (uint32_t)kRing) {
-                    const int l = (int)(p % kRing);
-                    return PredRow{__builtin_amdgcn_readlane(S.mOff, l), __builtin_amdgcn_readlane(S.mRm, l),
-                                   __builtin_amdgcn_readlane(S.mRarg, l)};
-                }
-                return pred_meta(z, r, p);
-            };
-            // band placement (SPEC.md §3.1)
-            off = 0;
-            if (np) {
-                const PredRow m0 = meta(p0);
-                int32_t bm = m0.rmax, barg = m0.rarg;
-                for (uint32_t s = 1; s < np; ++s) {
-                    const PredRow pm = meta(predp(s));
-                    if (pm.rmax > bm) bm = pm.rmax, barg = pm.rarg;
-                }
-                off = min(max(barg + 1 - kW / 2, 0), lim);
-            }
-            
-            // predecessor terms (SPEC.md §3.2)
-            int32_t Mh0 = kNeg, Mh1 = kNeg, Dv0 = kNeg, Dv1 = kNeg;
-            uint32_t ms0 = 0, ms1 = 0, ds0 = 0, ds1 = 0, dx0 = 0, dx1 = 0;
-            for (uint32_t s = 0; s < np; ++s) {
-                const uint32_t p = predp(s);
-                const PredRow pm = meta(p);
-                const int sh = off - pm.off;
-                int hA, hB, hC, dB, dC;
-                if (!SLOW || r - p <= (uint32_t)kRing) {
-                    const int32_t *row = z.lds + kLdsRing + (p % kRing) * 256;
-                    hA = cell_lds<0>(row, sh - 1, lane);
-                    hB = cell_lds<0>(row, sh, lane);
-                    hC = cell_lds<0>(row, sh + 1, lane);
-                    dB = cell_lds<2>(row, sh, lane);
-                    dC = cell_lds<2>(row, sh + 1, lane);
-                } else {
-                    const uint32_t sl = uni(__builtin_nontemporal_load(P<uint32_t>(z, z.L.sslot) + p));
-                    const int32_t *row = reinterpret_cast<const int32_t *>(z.ws + z.L.spill + (size_t)sl * (kW * 8 + 16));
-                    hA = cell_glb<0>(row, sh - 1, lane);
-                    hB = cell_glb<0>(row, sh, lane);
-                    hC = cell_glb<0>(row, sh + 1, lane);
-                    dB = cell_glb<2>(row, sh, lane);
-                    dC = cell_glb<2>(row, sh + 1, lane);
-                }
-                if (hA > Mh0) Mh0 = hA, ms0 = s;
-                if (hB > Mh1) Mh1 = hB, ms1 = s;
-                {
-                    const int a = hB + kO + kE, b = dB + kE;
-                    const int c = b > a ? b : a;
-                    if (c > Dv0) Dv0 = c, ds0 = s, dx0 = b > a ? 4u : 0u;
-                }
-                {
-                    const int a = hC + kO + kE, b = dC + kE;
-                    const int c = b > a ? b : a;
-                    if (c > Dv1) Dv1 = c, ds1 = s, dx1 = b > a ? 4u : 0u;
-                }
-            }
-            
-            if (off + kW <= (int32_t)m) o = row_cells<true>(z, S, r, off, m, base, Mh0, Mh1, Dv0, Dv1, dx0, dx1);
-            else o = row_cells<false>(z, S, r, off, m, base, Mh0, Mh1, Dv0, Dv1, dx0, dx1);
-            if (np > 1) {
-                // slots (SPEC.md §4 needs them); an MSRC cell's M slot is 0
-                const int32_t j0 = off + 2 * lane;
-                const bool ok0 = j0 < (int32_t)m, ok1 = j0 + 1 < (int32_t)m;
-                const uint32_t c0 = o.code & 15u, c1 = o.code >> 4;
-                const uint32_t s_m0 = ok0 && (c0 & 3u) != HC_MSRC ? ms0 : 0u;
-                const uint32_t s_m1 = ok1 && (c1 & 3u) != HC_MSRC ? ms1 : 0u;
-                const uint32_t s_d0 = ok0 ? ds0 : 0u, s_d1 = ok1 ? ds1 : 0u;
-                mi = S.nmulti - mi0;
-                st_slots[mi * 64 + lane] = s_m0 | (s_m1 << 8) | (s_d0 << 16) | (s_d1 << 24);
-                mi = S.nmulti++;
-            }
-            DP_STAMP(kPfRowB);  // general rows
-        }
-        // staged in LDS, flushed to HBM once per block
-        const uint32_t i = r - r0;
-        st_codes[i * 64 + lane] = (uint8_t)o.code;
-        if (lane == 0) {
-            st_meta[i * 2] = off;
-            st_meta[i * 2 + 1] = (int32_t)mi;
-        }
-        int32_t *row = z.lds + kLdsRing + (r % kRing) * 256;
-        row[lane] = o.H0;
-        row[64 + lane] = o.H1;
-        row[128 + lane] = o.D0;
-        row[192 + lane] = o.D1;
-        const bool mine = lane == (int)(r % kRing);
-        S.mOff = mine ? off : S.mOff;
-        S.mRm = mine ? o.rm : S.mRm;
-        S.mRarg = mine ? o.rarg : S.mRarg;
-        spill_mask |= ((info & kInfoSpill) ? 1u : 0u) << i;
-        S.pH0 = o.H0, S.pH1 = o.H1, S.pD0 = o.D0, S.pD1 = o.D1, S.pOff = off, S.pRm = o.rm, S.pRarg = o.rarg;
-    }
-    DP_STAMP(kPfRowE);
-    const uint32_t nm = S.nmulti - mi0;
-    if (S.nmulti > z.d.mcap) {
-        z.status = kErrMulti;
-        return;
-    }
-    // flush: codes (64 B/row), row meta, multi slots; registers f stay pinned
-    pin(f);
-    const uint32_t nrow = rend - r0;
-    uint8_t *codes = z.ws + z.L.codes + (size_t)r0 * 64;
-    uint2 *rmeta = reinterpret_cast<uint2 *>(z.ws + z.L.rmeta) + r0;
-    uint8_t *slots = z.ws + z.L.slots + (size_t)mi0 * 256;
-    f.code = reinterpret_cast<const uint4 *>(st_codes)[lane];
-    if ((uint32_t)lane * 16 < nrow * 64) reinterpret_cast<uint4 *>(codes)[lane] = f.code;
-    f.meta = reinterpret_cast<const uint2 *>(st_meta)[lane & (kBlk - 1)];
-    if ((uint32_t)lane < nrow) rmeta[lane] = f.meta;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const uint32_t chunk = (uint32_t)lane + 64u * c;
-        f.slot[c] = reinterpret_cast<const uint4 *>(st_slots)[chunk];
-        if (chunk * 16 < nm * 256) reinterpret_cast<uint4 *>(slots)[chunk] = f.slot[c];
-    }
-    // rows needed beyond the ring: copy them (still in the ring) to HBM
-    while (SLOW && spill_mask) {
-        const uint32_t i = __builtin_ctz(spill_mask);
-        spill_mask &= spill_mask - 1;
-        const uint32_t r = r0 + i;
-        if (S.nspill >= z.d.scap) {
-            z.status = kErrSpill;
-            return;
-        }
-        int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)S.nspill * (kW * 8 + 16));
-        const int32_t *row = z.lds + kLdsRing + (r % kRing) * 256;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rec[q * 64 + lane] = row[q * 64 + lane];
-        const int l = (int)(r % kRing);
-        const int32_t mo = __builtin_amdgcn_readlane(S.mOff, l), mr = __builtin_amdgcn_readlane(S.mRm, l),
-                      ma = __builtin_amdgcn_readlane(S.mRarg, l);
-        if (lane == 0) rec[256] = mo, rec[257] = mr, rec[258] = ma;
-        if (lane == 0) P<uint32_t>(z, z.L.sslot)[r] = S.nspill;
-        ++S.nspill;
-    }
 }
 
 // ----------------------------------------------------------------------------
@@ -694,17 +322,15 @@ constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
 constexpr int kBlkAB = 2;  // rows per A/B lockstep block
 static_assert(kPubSlots >= 2 * kBlkAB, "wave 1 reads the block before wave 0's");
-static_assert(kRingA * kRowW >= kRing * 256, "ring area too small for dp_block");
 static_assert(kRingA >= kRing + 2 * kBlkAB, "B reads predecessors up to kRing rows behind its row");
 
-static_assert(kLdsRing + kRingA * kRowW <= kLdsMeta, "ring overlaps the meta area");
 
 enum JobKind : int32_t { kJobExit = 0, kJobDp = 1 };
 struct DpJob {
     int32_t kind;
     uint32_t m, R, cur;
     // results (B)
-    uint32_t er, ej, nmulti;
+    uint32_t er, ej;
     int32_t status;
 };
 
@@ -719,26 +345,29 @@ struct PredAcc {
     uint32_t ms0, ms1, ds0, ds1, dx0, dx1;
 };
 
+// SLOTS: also track, per cell, the tag of the predecessor that gave Mh and D
+// (first in predecessor order on ties, SPEC.md §3.2) and D's ext bit; the
+// tag is the row distance r - p (or the slot index on rows flagged far)
 template <bool SLOTS>
-__device__ __forceinline__ void pred_fold(PredAcc &A, uint32_t s, int32_t hA, int32_t hB, int32_t hC, int32_t dB,
-                                          int32_t dC)
+__device__ __forceinline__ void pred_fold(PredAcc &A, uint32_t s, uint32_t tag, int32_t hA, int32_t hB, int32_t hC,
+                                          int32_t dB, int32_t dC)
 {
     const int32_t a0 = hB + (kO + kE), b0 = dB + kE, a1 = hC + (kO + kE), b1 = dC + kE;
     const int32_t c0 = max(a0, b0), c1 = max(a1, b1);
     if (s == 0) {
         A.Mh0 = hA, A.Mh1 = hB, A.Dv0 = c0, A.Dv1 = c1;
         if (SLOTS) {
-            A.ms0 = 0, A.ms1 = 0, A.ds0 = 0, A.ds1 = 0;
+            A.ms0 = A.ms1 = A.ds0 = A.ds1 = tag;
             A.dx0 = b0 > a0 ? 4u : 0u;
             A.dx1 = b1 > a1 ? 4u : 0u;
         }
     } else if (!SLOTS) {
         A.Mh0 = max(A.Mh0, hA), A.Mh1 = max(A.Mh1, hB), A.Dv0 = max(A.Dv0, c0), A.Dv1 = max(A.Dv1, c1);
     } else {
-        if (hA > A.Mh0) A.Mh0 = hA, A.ms0 = s;
-        if (hB > A.Mh1) A.Mh1 = hB, A.ms1 = s;
-        if (c0 > A.Dv0) A.Dv0 = c0, A.ds0 = s, A.dx0 = b0 > a0 ? 4u : 0u;
-        if (c1 > A.Dv1) A.Dv1 = c1, A.ds1 = s, A.dx1 = b1 > a1 ? 4u : 0u;
+        if (hA > A.Mh0) A.Mh0 = hA, A.ms0 = tag;
+        if (hB > A.Mh1) A.Mh1 = hB, A.ms1 = tag;
+        if (c0 > A.Dv0) A.Dv0 = c0, A.ds0 = tag, A.dx0 = b0 > a0 ? 4u : 0u;
+        if (c1 > A.Dv1) A.Dv1 = c1, A.ds1 = tag, A.dx1 = b1 > a1 ? 4u : 0u;
     }
 }
 
@@ -765,15 +394,15 @@ __device__ __forceinline__ void pred_cells(const int32_t *row, int32_t sh, int l
 
 // the predecessor terms of row r (np <= 4, every predecessor in the ring)
 template <bool SLOTS>
-__device__ __forceinline__ void pred_terms(const int32_t *ring, int32_t off, uint32_t np, uint32_t p0, uint32_t p1,
-                                           uint32_t p2, uint32_t p3, int32_t o0, int32_t o1, int32_t o2, int32_t o3,
-                                           int lane, PredAcc &A)
+__device__ __forceinline__ void pred_terms(const int32_t *ring, uint32_t r, int32_t off, uint32_t np, uint32_t p0,
+                                           uint32_t p1, uint32_t p2, uint32_t p3, int32_t o0, int32_t o1, int32_t o2,
+                                           int32_t o3, int lane, PredAcc &A)
 {
     const int32_t s0 = off - o0, s1 = off - o1, s2 = off - o2, s3 = off - o3;
     const bool inr = (uint32_t)(s0 + 3) <= 7u && (np < 2 || (uint32_t)(s1 + 3) <= 7u) &&
                      (np < 3 || (uint32_t)(s2 + 3) <= 7u) && (np < 4 || (uint32_t)(s3 + 3) <= 7u);
     if (np == 0) {
-        pred_fold<SLOTS>(A, 0, kNegH, kNegH, kNegH, kNeg, kNeg);
+        pred_fold<SLOTS>(A, 0, 0, kNegH, kNegH, kNegH, kNeg, kNeg);
     } else if (inr) {
         // every predecessor within the padded band: issue all reads (absent
         // slots re-read slot 0's row), then fold
@@ -787,25 +416,25 @@ __device__ __forceinline__ void pred_terms(const int32_t *ring, int32_t off, uin
         const int32_t c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
         const int32_t e0 = b2[0], e1 = b2[1], e2 = b2[2], e3 = b2[dd], e4 = b2[dd + 1];
         const int32_t g0 = b3[0], g1 = b3[1], g2 = b3[2], g3 = b3[dd], g4 = b3[dd + 1];
-        pred_fold<SLOTS>(A, 0, a0, a1, a2, a3, a4);
-        if (np > 1) pred_fold<SLOTS>(A, 1, c0, c1, c2, c3, c4);
-        if (np > 2) pred_fold<SLOTS>(A, 2, e0, e1, e2, e3, e4);
-        if (np > 3) pred_fold<SLOTS>(A, 3, g0, g1, g2, g3, g4);
+        pred_fold<SLOTS>(A, 0, r - p0, a0, a1, a2, a3, a4);
+        if (np > 1) pred_fold<SLOTS>(A, 1, r - p1, c0, c1, c2, c3, c4);
+        if (np > 2) pred_fold<SLOTS>(A, 2, r - p2, e0, e1, e2, e3, e4);
+        if (np > 3) pred_fold<SLOTS>(A, 3, r - p3, g0, g1, g2, g3, g4);
     } else {
         int32_t hA, hB, hC, dB, dC;
         pred_cells(ring + (p0 % kRingA) * kRowW, s0, lane, hA, hB, hC, dB, dC);
-        pred_fold<SLOTS>(A, 0, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, 0, r - p0, hA, hB, hC, dB, dC);
         if (np > 1) {
             pred_cells(ring + (p1 % kRingA) * kRowW, s1, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 1, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 1, r - p1, hA, hB, hC, dB, dC);
         }
         if (np > 2) {
             pred_cells(ring + (p2 % kRingA) * kRowW, s2, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 2, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 2, r - p2, hA, hB, hC, dB, dC);
         }
         if (np > 3) {
             pred_cells(ring + (p3 % kRingA) * kRowW, s3, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 3, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 3, r - p3, hA, hB, hC, dB, dC);
         }
     }
 }
@@ -814,8 +443,8 @@ __device__ __forceinline__ void pred_terms(const int32_t *ring, int32_t off, uin
 // within the ring; reads through the padded band when every shift is in
 // [-3, 4], else bounds-checked per cell
 template <int NP, bool SLOTS>
-__device__ __forceinline__ void pred_terms_n(const int32_t *ring, int32_t off, uint32_t p0, uint32_t p1, int32_t o0,
-                                             int32_t o1, int lane, PredAcc &A)
+__device__ __forceinline__ void pred_terms_n(const int32_t *ring, uint32_t r, int32_t off, uint32_t p0, uint32_t p1,
+                                             int32_t o0, int32_t o1, int lane, PredAcc &A)
 {
     const int32_t s0 = off - o0, s1 = off - o1;
     const bool inr = (uint32_t)(s0 + 3) <= 7u && (NP < 2 || (uint32_t)(s1 + 3) <= 7u);
@@ -827,15 +456,15 @@ __device__ __forceinline__ void pred_terms_n(const int32_t *ring, int32_t off, u
         const int32_t a0 = b0[0], a1 = b0[1], a2 = b0[2], a3 = b0[dd], a4 = b0[dd + 1];
         int32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
         if (NP > 1) c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
-        pred_fold<SLOTS>(A, 0, a0, a1, a2, a3, a4);
-        if (NP > 1) pred_fold<SLOTS>(A, 1, c0, c1, c2, c3, c4);
+        pred_fold<SLOTS>(A, 0, r - p0, a0, a1, a2, a3, a4);
+        if (NP > 1) pred_fold<SLOTS>(A, 1, r - p1, c0, c1, c2, c3, c4);
     } else {
         int32_t hA, hB, hC, dB, dC;
         pred_cells(ring + (p0 % kRingA) * kRowW, s0, lane, hA, hB, hC, dB, dC);
-        pred_fold<SLOTS>(A, 0, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, 0, r - p0, hA, hB, hC, dB, dC);
         if (NP > 1) {
             pred_cells(ring + (p1 % kRingA) * kRowW, s1, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 1, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 1, r - p1, hA, hB, hC, dB, dC);
         }
     }
 }
@@ -895,7 +524,7 @@ __device__ __forceinline__ void far_terms(const Z &z, uint32_t r, uint32_t np, i
         if (np) off = min(max(barg + 1 - kW / 2, 0), lim);
     }
     if (np == 0) {
-        pred_fold<SLOTS>(A, 0, kNegH, kNegH, kNegH, kNeg, kNeg);
+        pred_fold<SLOTS>(A, 0, 0, kNegH, kNegH, kNegH, kNeg, kNeg);
         return;
     }
     for (uint32_t s = 0; s < np; ++s) {
@@ -904,7 +533,7 @@ __device__ __forceinline__ void far_terms(const Z &z, uint32_t r, uint32_t np, i
         const int32_t *rec;
         far_meta(z, r, p, vOff, vKey, o, k, rec);
         far_cells(z, p, rec, off - o, lane, hA, hB, hC, dB, dC);
-        pred_fold<SLOTS>(A, s, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, s, s, hA, hB, hC, dB, dC);  // far rows: the tag is the slot
     }
 }
 
@@ -981,13 +610,13 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
             hA = S.H1, hB = wave_shl1(kNegH, S.H0), hC = wave_shl1(kNegH, S.H1);
             dB = wave_shl1(kNeg, S.D0), dC = wave_shl1(kNeg, S.D1);
         }
-        pred_fold<false>(A, 0, hA, hB, hC, dB, dC);
+        pred_fold<false>(A, 0, 0, hA, hB, hC, dB, dC);
     } else if (np == 1) {
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
         const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
         off = min(max(o0 + 127 - (k0 & 127) + 1 - kW / 2, 0), lim);
-        pred_terms_n<1, false>(ring, off, p0, p0, o0, o0, lane, A);
+        pred_terms_n<1, false>(ring, r, off, p0, p0, o0, o0, lane, A);
     } else if (np == 2) {
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
         const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
@@ -999,7 +628,7 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
         const bool second = (k1 >> 7) > (k0 >> 7);
         const int32_t ko = second ? k1 : k0, oo = second ? o1 : o0;
         off = min(max(oo + 127 - (ko & 127) + 1 - kW / 2, 0), lim);
-        pred_terms_n<2, false>(ring, off, p0, p1, o0, o1, lane, A);
+        pred_terms_n<2, false>(ring, r, off, p0, p1, o0, o1, lane, A);
     } else {
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
         const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
@@ -1021,13 +650,16 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
             if (np > 3 && (k3 >> 7) > bm) bm = k3 >> 7, barg = o3 + 127 - (k3 & 127);
             off = min(max(barg + 1 - kW / 2, 0), lim);
         }
-        pred_terms<false>(ring, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
+        pred_terms<false>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
     }
     off_o = off, Mh0 = A.Mh0, Mh1 = A.Mh1, Dv0 = A.Dv0, Dv1 = A.Dv1;
 }
 
-// wave 0: one DP row (SPEC.md §3.1-§3.4 values)
-__device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim, const LaneK &c)
+// wave 0: one DP row (SPEC.md §3.1-§3.4 values).  FULL: m >= W, every band
+// cell is a read position; else (m < W, off == 0) cells t >= m are invalid:
+// H = kNegH, D = kNeg there, and they take no part in the row maximum.
+template <bool FULL>
+__device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim, uint32_t m, const LaneK &c)
 {
     const int lane = lane_id();
     const int li = (int)(r & 63u);
@@ -1059,10 +691,19 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const int32_t hp0 = max(M0, Dv0), hp1 = max(M1, Dv1);
     const int32_t X0 = hp0 + c.L4;
     int32_t incl = max(X0, hp1 + c.L4 + 2);
-    int32_t rk = max((hp0 << 7) | c.kc0, (hp1 << 7) | c.kc1);
+    int32_t rk0 = (hp0 << 7) | c.kc0, rk1 = (hp1 << 7) | c.kc1;
+    if (!FULL) {
+        if ((uint32_t)c.L2 >= m) rk0 = INT32_MIN, Dv0 = kNeg;
+        if ((uint32_t)c.L2 + 1 >= m) rk1 = INT32_MIN, Dv1 = kNeg;
+    }
+    int32_t rk = max(rk0, rk1);
     wave_incl_max2(incl, rk);
     const int32_t Pex = wave_shr1(kNeg, incl);
-    const int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(max(Pex, X0) + c.cI1, hp1);
+    int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(max(Pex, X0) + c.cI1, hp1);
+    if (!FULL) {
+        if ((uint32_t)c.L2 >= m) nH0 = kNegH;
+        if ((uint32_t)c.L2 + 1 >= m) nH1 = kNegH;
+    }
     const int32_t key = __builtin_amdgcn_readlane(rk, 63);
     // ring row, {M0, M1, Pex} for wave 1, meta window
     int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kHc + c.L2);
@@ -1094,14 +735,15 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
 }
 
 // wave 0: rows [r0, r0 + kBlkAB)
+template <bool FULL>
 __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t m)
 {
     const int lane = lane_id();
-    const int32_t lim = (int32_t)m - kW;
+    const int32_t lim = FULL ? (int32_t)m - kW : 0;
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
-    dpA_row(z, S, r0, lim, c);
-    if (r0 + 1 < z.R) dpA_row(z, S, r0 + 1, lim, c);
+    dpA_row<FULL>(z, S, r0, lim, m, c);
+    if (r0 + 1 < z.R) dpA_row<FULL>(z, S, r0 + 1, lim, m, c);
     z.lds[kLdsOffRing + lane] = S.vOff;  // band offsets of the last 64 rows for wave 1
     recwin_end(S.W, r0);
 }
@@ -1109,15 +751,14 @@ __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t
 struct BState {
     int32_t bE;       // best free-end value of this lane's cells
     uint32_t bKey;    // its row * 2 + cell
-    uint32_t vMi;     // lane (q & 63): multi-slot ordinal of row q or kNone
-    uint32_t nmulti, mg0;  // multi rows so far / at the start of the flush group
+    uint32_t vFar;    // lane (q & 63): row q's cell tags are predecessor slots (kInfoFar rows)
     RecWin W;
     FlushBuf fa, fb;
 };
 
 // wave 1: the predecessor terms of a row that does not have exactly one
 // in-band predecessor (0 or >= 2 predecessors, or a far band shift)
-__device__ __forceinline__ void dpB_cold(const Z &z, const BState &S, uint32_t r, uint32_t info, int32_t off,
+__device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint32_t info, int32_t off,
                                          int32_t vOff, PredAcc &A)
 {
     const int lane = lane_id();
@@ -1126,7 +767,8 @@ __device__ __forceinline__ void dpB_cold(const Z &z, const BState &S, uint32_t r
     const int32_t *ring = z.lds + kLdsRing;
     if (info & kInfoFar) {
         int32_t o = off;
-        // the keys of rows in the ring are wave 0's; band placement is not redone here
+        // band placement is wave 0's; the cell tags are predecessor slots (6 bits)
+        if (np > 63) z.status = kErrInDegree;
         far_terms<true>(z, r, np, vOff, 0, 0, false, o, A);
         return;
     }
@@ -1135,19 +777,23 @@ __device__ __forceinline__ void dpB_cold(const Z &z, const BState &S, uint32_t r
     const int32_t o0 = __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
     const int32_t o1 = __builtin_amdgcn_readlane(vOff, (int)(p1 & 63u));
     if (np == 2) {
-        pred_terms_n<2, true>(ring, off, p0, p1, o0, o1, lane, A);
+        pred_terms_n<2, true>(ring, r, off, p0, p1, o0, o1, lane, A);
     } else if (np == 1) {
-        pred_terms_n<1, true>(ring, off, p0, p0, o0, o0, lane, A);
+        pred_terms_n<1, true>(ring, r, off, p0, p0, o0, o0, lane, A);
     } else {
         const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p2, li);
         const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p3, li);
         const int32_t o2 = __builtin_amdgcn_readlane(vOff, (int)(p2 & 63u));
         const int32_t o3 = __builtin_amdgcn_readlane(vOff, (int)(p3 & 63u));
-        pred_terms<true>(ring, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
+        pred_terms<true>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
     }
 }
 
-// wave 1: the decision bits of one row (wave 0 wrote its ring row and {M, Pex})
+// wave 1: the decision bits of one row (wave 0 wrote its ring row and
+// {M, Pex}).  Output per cell, 16 bits: code (SPEC.md §3.4) | M tag << 4 |
+// D tag << 10; a tag is the distance to the predecessor the cell's M / D
+// came from (its slot on rows flagged far), staged as one word per lane.
+template <bool FULL>
 __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m, int32_t lim, int32_t vOff,
                                         const LaneK &c)
 {
@@ -1163,19 +809,17 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     A.Dv0 = Dv.x, A.Dv1 = Dv.y;
     const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
     const int32_t sh = off - __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
-    bool multi = false;
     if (__builtin_expect(np == 1 && (uint32_t)(sh + 3) <= 7u && !(info & kInfoFar), 1)) {
         // one predecessor in the padded band: its H at t-1, t, t+1; D-ext is
         // D > H + O + E (D = max(H + O + E, D' + E))
         const int32_t *b = z.lds + kLdsRing + (p0 % kRingA) * kRowW + (kHc - 1) + c.L2 + sh;
         const int32_t hA = b[0], hB = b[1], hC = b[2];
         A.Mh0 = hA, A.Mh1 = hB;
-        A.ms0 = A.ms1 = A.ds0 = A.ds1 = 0;
+        A.ms0 = A.ms1 = A.ds0 = A.ds1 = r - p0;
         A.dx0 = A.Dv0 > hB + (kO + kE) ? 4u : 0u;
         A.dx1 = A.Dv1 > hC + (kO + kE) ? 4u : 0u;
     } else {
         dpB_cold(z, S, r, info, off, vOff, A);
-        multi = np > 1;
     }
     const int32_t srcu = c.src0 + kE * off;
     const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
@@ -1190,67 +834,65 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
     const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
-    const uint32_t code = (hc0 | A.dx0 | iext0) | ((hc1 | A.dx1 | iext1) << 4);
+    uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 << 4) | (A.ds0 << 10);
+    uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 << 4) | (A.ds1 << 10);
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
-    // H' at j = m - 1 (lane 63, cell 1 when off == lim)
+    // H' at j = m - 1
     const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
-    const int32_t e0 = X0 + eb;
-    const int32_t e1 = X1 + eb + ((off == lim && lane == 63) ? 3 : 0);
+    int32_t e0 = X0 + eb;
+    int32_t e1 = X1 + eb;
+    if (FULL) {
+        e1 += (off == lim && lane == 63) ? 3 : 0;
+    } else {
+        if ((uint32_t)c.L2 == m - 1) e0 += 3;
+        if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
+        if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
+        if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
+    }
     if (e0 > S.bE) S.bE = e0, S.bKey = r * 2;
     if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1;
-    uint32_t mi = kNone;
-    if (multi) {
-        // slots of a multi-predecessor row (SPEC.md §4); an MSRC cell's M slot is 0
-        const uint32_t s_m0 = mp0 ? A.ms0 : 0u, s_m1 = mp1 ? A.ms1 : 0u;
-        reinterpret_cast<uint32_t *>(z.lds + kLdsStSlots)[(S.nmulti - S.mg0) * 64 + lane] =
-            s_m0 | (s_m1 << 8) | (A.ds0 << 16) | (A.ds1 << 24);
-        mi = S.nmulti++;
-    }
-    reinterpret_cast<uint8_t *>(z.lds + kLdsStCodes)[(r & 15u) * 64 + lane] = (uint8_t)code;
-    S.vMi = (uint32_t)writelane((int)S.vMi, (int)mi, li);
+    z.lds[kLdsStRec + (r & 15u) * 64 + lane] = (int32_t)(w0 | (w1 << 16));
+    S.vFar = (uint32_t)writelane((int)S.vFar, (int)(info & kInfoFar), li);
 }
 
-// wave 1: rows [r0, r0 + kBlkAB), then the 16-row group's flush
+// wave 1: rows [r0, r0 + kBlkAB), then the 16-row group's flush: cell
+// records (256 B/row) and row meta {band offset, far flag}
+template <bool FULL>
 __device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t m, FlushBuf &f)
 {
     const int lane = lane_id();
     const uint32_t R = z.R;
-    const int32_t lim = (int32_t)m - kW;
+    const int32_t lim = FULL ? (int32_t)m - kW : 0;
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
     const int32_t vOff = z.lds[kLdsOffRing + lane];
-    dpB_row(z, S, r0, m, lim, vOff, c);
-    if (r0 + 1 < R) dpB_row(z, S, r0 + 1, m, lim, vOff, c);
+    dpB_row<FULL>(z, S, r0, m, lim, vOff, c);
+    if (r0 + 1 < R) dpB_row<FULL>(z, S, r0 + 1, m, lim, vOff, c);
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
     recwin_end(S.W, r0);
     if ((r0 & 15u) == 16u - kBlkAB || rend == R) {
-        if (S.nmulti > z.d.mcap) z.status = kErrMulti;
         pin(f);
         const uint32_t g0 = r0 & ~15u;
-        const uint32_t nm = z.status ? 0u : S.nmulti - S.mg0;
         const uint32_t nrow = z.status ? 0u : rend - g0;
-        f.code = reinterpret_cast<const uint4 *>(z.lds + kLdsStCodes)[lane];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            f.slot[k] = reinterpret_cast<const uint4 *>(z.lds + kLdsStSlots)[(uint32_t)lane + 64u * k];
-        f.meta = make_uint2((uint32_t)vOff, S.vMi);
-        const auto rc = brsrc(z.ws + z.L.codes + (size_t)g0 * 64, nrow * 64);
+            f.slot[k] = reinterpret_cast<const uint4 *>(z.lds + kLdsStRec)[(uint32_t)lane + 64u * k];
+        f.meta = make_uint2((uint32_t)vOff, S.vFar);
+        const auto rc = brsrc(z.ws + z.L.codes + (size_t)g0 * 256, nrow * 256);
         const auto rm = brsrc(reinterpret_cast<uint2 *>(z.ws + z.L.rmeta) + g0, nrow * 8);
-        const auto rs = brsrc(z.ws + z.L.slots + (size_t)S.mg0 * 256, nm * 256);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{f.code.x, f.code.y, f.code.z, f.code.w}, rc, lane * 16, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(v4u{f.slot[k].x, f.slot[k].y, f.slot[k].z, f.slot[k].w}, rc,
+                                                   ((uint32_t)lane + 64u * k) * 16u, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b64(v2u{f.meta.x, f.meta.y}, rm, (uint32_t)(lane - (int)(g0 & 63u)) * 8u,
                                               0, 0);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            __builtin_amdgcn_raw_buffer_store_b128(v4u{f.slot[k].x, f.slot[k].y, f.slot[k].z, f.slot[k].w}, rs,
-                                                   ((uint32_t)lane + 64u * k) * 16u, 0, 0);
-        S.mg0 = S.nmulti;
     }
 }
 
 __device__ __forceinline__ uint32_t dp_nblk(uint32_t R) { return (R + kBlkAB - 1) / kBlkAB; }
 
 // wave 0's side of a two-wave DP (wave 1 is in dp_helper)
+template <bool FULL>
 __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
 {
     const int lane = lane_id();
@@ -1274,26 +916,27 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
     unsigned long long t_prev = stamp();
 #endif
     for (uint32_t b = 0; b <= nblk; ++b) {
-        if (b < nblk) dpA_block(z, S, b * kBlkAB, m);
+        if (b < nblk) dpA_block<FULL>(z, S, b * kBlkAB, m);
         DP_STAMP(kPfAbusy);
         lds_barrier();
         DP_STAMP(kPfAwait);
     }
-    er_out = job->er;
-    ej_out = job->ej;
-    if (job->status && !z.status) z.status = job->status;
-    z.cells += (unsigned long long)z.R * (uint32_t)kW;
+    er_out = uni(job->er);
+    ej_out = uni(job->ej);
+    const int32_t bst = uni(job->status);
+    if (bst && !z.status) z.status = bst;
+    z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
 }
 
 // wave 1's side of one DP
+template <bool FULL>
 __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m)
 {
     const int lane = lane_id();
     BState S;
-    S.bE = INT32_MIN, S.bKey = 0, S.vMi = kNone, S.nmulti = 0, S.mg0 = 0;
+    S.bE = INT32_MIN, S.bKey = 0, S.vFar = 0;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
-    S.fa.code = S.fb.code = make_uint4(0, 0, 0, 0);
     S.fa.meta = S.fb.meta = make_uint2(0, 0);
 #pragma unroll
     for (int c = 0; c < 4; ++c) S.fa.slot[c] = S.fb.slot[c] = make_uint4(0, 0, 0, 0);
@@ -1304,8 +947,8 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m)
     for (uint32_t b = 0; b <= nblk; ++b) {
         if (b >= 1 && !z.status) {
             const uint32_t bb = b - 1;
-            if ((bb * kBlkAB >> 4) & 1u) dpB_block(z, S, bb * kBlkAB, m, S.fb);
-            else dpB_block(z, S, bb * kBlkAB, m, S.fa);
+            if ((bb * kBlkAB >> 4) & 1u) dpB_block<FULL>(z, S, bb * kBlkAB, m, S.fb);
+            else dpB_block<FULL>(z, S, bb * kBlkAB, m, S.fa);
         }
         if (b == nblk) {
             // results: lexicographic (max score, min row, min j) over the lanes
@@ -1321,7 +964,7 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m)
             uint32_t ej = 0;
             if (!z.status) ej = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin].x + (uint32_t)tmin;
             volatile DpJob *job = dp_job(z);
-            if (lane == 0) job->er = (uint32_t)rmin, job->ej = ej, job->status = z.status, job->nmulti = S.nmulti;
+            if (lane == 0) job->er = (uint32_t)rmin, job->ej = ej, job->status = z.status;
         }
         DP_STAMP(kPfBbusy);
         lds_barrier();
@@ -1335,12 +978,14 @@ __device__ __forceinline__ void dp_helper(Z &z)
     for (;;) {
         __syncthreads();  // J: job posted
         volatile DpJob *job = dp_job(z);
-        const int32_t kind = job->kind;
+        const int32_t kind = uni(job->kind);
         if (kind == kJobExit) break;
-        z.R = job->R;
-        z.cur = (int)job->cur;
+        z.R = uni(job->R);
+        z.cur = uni((int)job->cur);
         z.status = kOk;
-        dp_wave_b(z, job->m);
+        const uint32_t m = uni(job->m);
+        if (m >= (uint32_t)kW) dp_wave_b<true>(z, m);
+        else dp_wave_b<false>(z, m);
     }
 }
 
@@ -1357,71 +1002,35 @@ __device__ __forceinline__ void dp_helper_exit(Z &z)
 
 __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
 {
-    if (m >= (uint32_t)kW && m < (1u << 22)) {
-        z.pf[kPfTwRows] += z.R;
-        dp_two_wave(z, m, er_out, ej_out);
+    er_out = ej_out = 0;
+    if (m >= (1u << 22)) {  // keys of the row-max scan need |H'| < 2^24
+        z.status = kErrReadLen;
         return;
     }
-    z.pf[kPfSwRows] += z.R;
-    DpState S;
-    S.bE = INT32_MIN, S.bKey = 0, S.nmulti = 0, S.nspill = 0;
-    S.pH0 = S.pH1 = S.pD0 = S.pD1 = kNeg, S.pOff = 0, S.pRm = 0, S.pRarg = 0;
-    S.mOff = S.mRm = S.mRarg = 0;
-    S.cur = RowPre{0, 0, 0, 0, 0, 0};
-    S.nxt = S.cur;
-    FlushBuf fa, fb;
-    fa.code = fb.code = make_uint4(0, 0, 0, 0);
-    fa.meta = fb.meta = make_uint2(0, 0);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) fa.slot[c] = fb.slot[c] = make_uint4(0, 0, 0, 0);
-    const uint32_t nblk = (z.R + kBlk - 1) / kBlk;
-    if (z.slow) {
-        for (uint32_t blk = 0; blk < nblk && !z.status; blk += 2) {
-            dp_block<true>(z, S, blk, m, fa);
-            if (z.status) break;
-            dp_block<true>(z, S, blk + 1, m, fb);
-        }
-    } else {
-        for (uint32_t blk = 0; blk < nblk && !z.status; blk += 2) {
-            dp_block<false>(z, S, blk, m, fa);
-            if (z.status) break;
-            dp_block<false>(z, S, blk + 1, m, fb);
-        }
-    }
-    pin(fa);
-    pin(fb);
-    // lexicographic (max score, min row, min j) over the lanes' candidates;
-    // within one row a smaller lane (and t0 before t1) is a smaller j
-    const int32_t best = wave_max(S.bE);
-    const uint32_t rsel = S.bE == best ? S.bKey >> 1 : 0x7FFFFFFFu;
-    const int32_t rmin = wave_min((int32_t)rsel);
-    const bool mine = S.bE == best && (S.bKey >> 1) == (uint32_t)rmin;
-    const uint32_t tsel = mine ? 2u * (uint32_t)lane_id() + (S.bKey & 1u) : 0x7FFFFFFFu;
-    const int32_t tmin = wave_min((int32_t)tsel);
-    er_out = (uint32_t)rmin;
-    wsync();
-    const uint2 em = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin];  // flushed band offset of the end row
-    ej_out = em.x + (uint32_t)tmin;
-    z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
-    wsync();
+    z.pf[kPfTwRows] += z.R;
+    if (m >= (uint32_t)kW) dp_two_wave<true>(z, m, er_out, ej_out);
+    else dp_two_wave<false>(z, m, er_out, ej_out);
 }
 
 // ----------------------------------------------------------------------------
-// SPEC.md §4: traceback into one event per read base.  The path walks rows
-// backwards; blocks of kTbRows rows (band offsets, first two predecessors,
-// their code rows and the slots of their multi-predecessor rows) are staged
-// into LDS by the whole wave, then lane 0 walks inside LDS.
+// SPEC.md §4: traceback into one event per read base.  The wave walks the
+// 16-bit cell records of the two-wave DP (code | M tag << 4 | D tag << 10)
+// backwards in 32-row blocks staged in LDS (the next block is loaded while
+// the current one is walked).  One uniform ds_read per step; the band
+// offsets of the current and previous block sit in one VGPR (readlane);
+// events collect in a VGPR, lane j & 63, stored 64 at a time.
 // ----------------------------------------------------------------------------
 constexpr uint32_t kTbRows = 32;
+constexpr uint32_t kTbBufWords = kTbRows * 64;  // 32 rows x 256 B
 
-// Traceback step tables indexed by (state << 4 | cell code), state 0 = H,
-// 1 = D, 2 = I; code = hcode | D-ext << 2 | iext << 3 (SPEC.md §3.4, §4).
-// kTbAct[state]: 4 bits per code {emit, move to predecessor, j -= 1, stop
-// (MSRC)}; kTbNext[state]: next state (4-bit fields).
+// Traceback step tables indexed by (state, cell code), state 0 = H, 1 = D,
+// 2 = I; code = hcode | D-ext << 2 | I-ext << 3 (SPEC.md §3.4, §4).
+// kTbAct[state]: 4 bits per code {emit, move to the predecessor, j -= 1,
+// stop (MSRC)}; kTbNext[state]: the next state (4-bit fields).
 constexpr uint32_t tb_act(uint32_t st, uint32_t c)
 {
     return st == 0 ? ((c & 3u) == 0 ? 0x7u : (c & 3u) == 1 ? 0x9u : 0u)  // MPRED: emit+pred+dj, MSRC: emit+stop
-         : st == 1 ? 0x2u                                               // D: move to the D slot's predecessor
+         : st == 1 ? 0x2u                                               // D: move to the D tag's predecessor
                    : 0x5u;                                              // I: emit INS, j -= 1
 }
 constexpr uint32_t tb_next(uint32_t st, uint32_t c)
@@ -1438,157 +1047,160 @@ constexpr uint64_t tb_table(uint32_t st, bool act)
 }
 constexpr uint64_t kTbAct[3] = {tb_table(0, true), tb_table(1, true), tb_table(2, true)};
 constexpr uint64_t kTbNext[3] = {tb_table(0, false), tb_table(1, false), tb_table(2, false)};
+static_assert(2 * kTbBufWords + 128 <= kRingA * kRowW, "traceback buffers live in the DP ring area");
+
+struct TbBlock {
+    uint4 v[8];  // this lane's 128 B of a 32-row block of records
+    uint2 mt;    // lane l < 32: rmeta {band offset, far} of the block's row l
+};
+
+__device__ __forceinline__ void tb_fetch(const Z &z, uint32_t bi, TbBlock &x)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t r0 = bi * kTbRows;
+    const uint32_t n = r0 < z.R ? min(z.R - r0, kTbRows) : 0u;
+    const auto rc = brsrc(z.ws + z.L.codes + (size_t)r0 * 256, n * 256);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const v4u q = __builtin_amdgcn_raw_buffer_load_b128(rc, (lane + 64u * k) * 16u, 0, 0);
+        x.v[k] = make_uint4(q.x, q.y, q.z, q.w);
+    }
+    const auto rm = brsrc(reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta) + r0, n * 8);
+    const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rm, lane * 8u, 0, 0);
+    x.mt = make_uint2(q.x, q.y);
+}
+
+// records to LDS buffer `buf`, the row meta words (offset | far << 31) to its tail
+__device__ __forceinline__ uint32_t tb_put(const Z &z, const TbBlock &x, uint32_t buf)
+{
+    uint4 *d = reinterpret_cast<uint4 *>(z.lds + buf * kTbBufWords);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[lane_id() + 64u * k] = x.v[k];
+    const uint32_t w = x.mt.x | (x.mt.y ? 0x80000000u : 0u);
+    z.lds[2 * kTbBufWords + buf * 64 + lane_id()] = (int32_t)w;
+    return w;
+}
 
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
     const uint32_t lane = lane_id();
     uint32_t *ev = P<uint32_t>(z, z.L.ev);
     for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
-    const uint32_t *poff = G_poff(z, z.cur);
-    const uint32_t *pred = G_pred(z, z.cur);
-    const uint2 *rmeta = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta);
-    const uint8_t *codes = z.ws + z.L.codes;
-    const uint8_t *slots = z.ws + z.L.slots;
-    // LDS: per block row two 16-B records {roff, slot-row or kNone, np, poff}
-    // and {p0, p1, p2, p3}; then codes, slots and the staged events
-    uint4 *tbr = reinterpret_cast<uint4 *>(z.lds);  // [kTbRows][2]
-    uint8_t *tbc = reinterpret_cast<uint8_t *>(z.lds + 256);              // kTbRows x 64 B codes
-    uint8_t *tbs = reinterpret_cast<uint8_t *>(z.lds + 256 + 16 * kTbRows);  // slots of the block's multi rows
-    uint32_t *evs = reinterpret_cast<uint32_t *>(z.lds + 256 + 16 * kTbRows + 64 * kTbRows);  // walk output
-    constexpr uint32_t kEvStage = 2048;
-    static_assert(256 + 16 * kTbRows + 64 * kTbRows + kEvStage <= (uint32_t)kLdsFixedWords, "traceback LDS");
-    uint32_t r = er, lead_row = 0, lead_j = 0;
-    int32_t j = (int32_t)ej, st = 0, err = 0, done = 0;
+    uint32_t r = er, bi = er / kTbRows, buf = 0;
+    int32_t j = (int32_t)ej;
+    TbBlock nx;
+    tb_fetch(z, bi, nx);
+    uint32_t vmeta = tb_put(z, nx, buf);
+    if (bi) tb_fetch(z, bi - 1, nx);
+    const auto rev = brsrc(ev, m * 4);
+    uint32_t vev = 0;                      // events of bases [chunk, chunk + 64), lane = base & 63
+    int32_t chunk = j & ~63;
+    uint32_t top = (uint32_t)(j - chunk);  // highest lane of the chunk that is ours (the rest are INS events)
+    uint32_t lead_row = 0, lead_j = 0;
+    int32_t err = 0;
     uint32_t guard = 0;
     const uint32_t glim = z.R * 2u + m * 2u + 16u;
-#ifdef CCSX_DP_STAMPS
-    unsigned long long t_prev = stamp();
-#endif
-    while (!done) {
-        const uint32_t blo = r >= kTbRows - 1 ? r - (kTbRows - 1) : 0u;
-        const uint32_t nr = r - blo + 1;
-        uint32_t mi = kNone, po = 0, np = 0, roff = 0;
-        if (lane < nr) {
-            const uint32_t row = blo + lane;
-            po = poff[row];
-            np = poff[row + 1] - po;
-            const uint2 mt = rmeta[row];
-            roff = mt.x;
-            mi = mt.y;
+    const uint32_t *poff = G_poff(z, z.cur);
+    const uint32_t *pred = G_pred(z, z.cur);
+    // the record of cell (r, j); moves to r's block first
+    auto cell = [&](uint32_t &mt) -> uint32_t {
+        if (r < bi * kTbRows) {
+            const uint32_t nb = r / kTbRows;
+            if (nb + 1 != bi) tb_fetch(z, nb, nx);
+            bi = nb;
+            buf ^= 1u;
+            vmeta = tb_put(z, nx, buf);
+            if (bi) tb_fetch(z, bi - 1, nx);
         }
-        const uint32_t p0 = lane < nr && np > 0 ? pred[po] : 0u;
-        const uint32_t p1 = lane < nr && np > 1 ? pred[po + 1] : 0u;
-        const uint32_t p2 = lane < nr && np > 2 ? pred[po + 2] : 0u;
-        const uint32_t p3 = lane < nr && np > 3 ? pred[po + 3] : 0u;
-        // multi ordinals are increasing in row order: the block's slots are contiguous
-        const uint32_t mi_lo = (uint32_t)wave_min((int32_t)(mi == kNone ? 0x7FFFFFFFu : mi));
-        const uint32_t mi_hi = (uint32_t)wave_max((int32_t)(mi == kNone ? 0u : mi + 1));
-        const uint32_t nms = mi_lo == 0x7FFFFFFFu ? 0u : mi_hi - mi_lo;
-        if (lane < nr) {
-            tbr[lane * 2] = make_uint4(roff, mi == kNone ? kNone : mi - mi_lo, np, po);
-            tbr[lane * 2 + 1] = make_uint4(p0, p1, p2, p3);
+        mt = (uint32_t)__builtin_amdgcn_readlane((int)vmeta, (int)(r - bi * kTbRows));
+        const int32_t t = j - (int32_t)(mt & 0x7FFFFFFFu);
+        const uint16_t *rb = reinterpret_cast<const uint16_t *>(z.lds + buf * kTbBufWords);
+        return uni((uint32_t)rb[(r - bi * kTbRows) * 128u + (uint32_t)t]);
+    };
+    auto emit = [&](uint32_t e) { vev = (uint32_t)writelane((int)vev, (int)e, j & 63); };
+    auto step_j = [&]() {
+        if ((j & 63) == 0) {
+            __builtin_amdgcn_raw_buffer_store_b32(vev, rev, lane <= top ? (uint32_t)(chunk + (int32_t)lane) * 4u : ~0u,
+                                                  0, 0);
+            chunk -= 64;
+            top = 63;
         }
-        for (uint32_t o = lane * 16; o < nr * 64; o += 1024)
-            *reinterpret_cast<uint4 *>(tbc + o) = *reinterpret_cast<const uint4 *>(codes + (size_t)blo * 64 + o);
-        for (uint32_t o = lane * 16; o < nms * 256; o += 1024)
-            *reinterpret_cast<uint4 *>(tbs + o) = *reinterpret_cast<const uint4 *>(slots + (size_t)mi_lo * 256 + o);
-        wsync();
-        DP_STAMP(kPfSpare0);
-        // The wave walks the block.  In state H a probe first follows the
-        // diagonal run in one go: lane i checks that cell (r - i, j - i) is
-        // MPRED and that its predecessor is row r - i - 1; the run ends at the
-        // first lane that fails.  Then one table-driven step (kTbAct) takes the
-        // cell where the run ended.  Events are staged in LDS (a global store
-        // per step would stall the next step on its store-data wait) and
-        // flushed by the wave.
-        const int32_t jhi = j;
-        uint32_t nev = 0, far_pred = kNone;
-        {
-            uint32_t rr = r, stt = (uint32_t)st, ne = 0, g = guard;
-            int32_t jj = j;
-            while (rr >= blo && ne + 65 <= kEvStage) {
-                if (++g > glim) {
-                    err = kErrTrace;
-                    done = 1;
-                    break;
-                }
-                if (stt == 0) {
-                    const int32_t rowi = (int32_t)rr - (int32_t)lane, ji = jj - (int32_t)lane;
-                    bool ok = rowi >= (int32_t)blo && ji >= 0;
-                    const uint32_t ri = ok ? (uint32_t)rowi - blo : 0u;
-                    const uint4 rec = tbr[ri * 2];
-                    const uint32_t t = (uint32_t)ji - rec.x;
-                    ok = ok && t < (uint32_t)kW;
-                    const uint32_t tc = t & (uint32_t)(kW - 1);
-                    const uint32_t c = (tbc[ri * 64 + (tc >> 1)] >> ((tc & 1u) << 2)) & 15u;
-                    const uint32_t sl = rec.y != kNone ? tbs[rec.y * 256 + (tc >> 1) * 4 + (tc & 1u)] : 0u;
-                    const uint4 pp = tbr[ri * 2 + 1];
-                    const uint32_t prow = sl == 0 ? pp.x : sl == 1 ? pp.y : sl == 2 ? pp.z : pp.w;
-                    ok = ok && (c & 3u) == HC_MPRED && sl < 4 && prow + 1 == (uint32_t)rowi;
-                    const uint64_t bad = ~ballot(ok);
-                    const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
-                    if (lane < k) evs[ne + lane] = (EV_ALN << 30) | (uint32_t)rowi;
-                    ne += k;
-                    rr -= k;
-                    jj -= (int32_t)k;
-                    if (rr < blo || rr == 0xFFFFFFFFu) break;
-                }
-                const uint32_t ri = rr - blo;
-                const uint4 rec = tbr[ri * 2];
-                const uint32_t t = (uint32_t)jj - rec.x;
-                const uint32_t c = uni((uint32_t)(tbc[ri * 64 + (t >> 1)] >> ((t & 1u) << 2)) & 15u);
-                const uint64_t ta = stt == 0 ? kTbAct[0] : stt == 1 ? kTbAct[1] : kTbAct[2];
-                const uint64_t tn = stt == 0 ? kTbNext[0] : stt == 1 ? kTbNext[1] : kTbNext[2];
-                const uint32_t act = (uint32_t)(ta >> (c * 4)) & 15u;  // emit | pred | dj | stop
-                const uint32_t nst = (uint32_t)(tn >> (c * 4)) & 3u;
-                if (act & 1u) {
-                    if (lane == 0) evs[ne] = ((stt == 2 ? EV_INS : EV_ALN) << 30) | rr;
-                    ++ne;
-                }
-                if (act & 8u) {
-                    lead_row = rr;
-                    lead_j = (uint32_t)jj;
-                    done = 1;
-                    break;
-                }
-                jj -= (int32_t)((act >> 2) & 1u);
-                if (act & 2u) {
-                    const uint32_t s = rec.y != kNone
-                                           ? uni((uint32_t)tbs[rec.y * 256 + (t >> 1) * 4 + (stt == 1 ? 2u : 0u) + (t & 1u)])
-                                           : 0u;
-                    if (s >= 4) {
-                        far_pred = rec.w + s;
-                        stt = nst;
-                        break;
-                    }
-                    const uint4 pp = tbr[ri * 2 + 1];
-                    rr = uni(s == 0 ? pp.x : s == 1 ? pp.y : s == 2 ? pp.z : pp.w);
-                }
-                stt = nst;
+        --j;
+    };
+    auto to_pred = [&](uint32_t mt, uint32_t tag) {
+        if (mt & 0x80000000u) r = uni(pred[uni(poff[r]) + tag]);  // far row: the tag is a slot
+        else r -= tag;
+    };
+    uint32_t mt;
+    uint32_t rec = cell(mt);
+    for (;;) {
+        if (++guard > glim) {
+            err = kErrTrace;
+            break;
+        }
+        const uint32_t hc = rec & 3u;
+        if (hc == HC_MPRED) {  // state H
+            emit((EV_ALN << 30) | r);
+            if ((rec & 0x3F3u) == 0x10u && !(mt & 0x80000000u) && (j & 63) != 0 && r > bi * kTbRows) {
+                // diagonal run: lane i checks that cell (r-1-i, j-1-i) is MPRED to
+                // the row above it, inside this block and this event chunk; the
+                // run's events go into vev by one lane permutation
+                const int32_t i = (int32_t)lane;
+                const int32_t ri = (int32_t)(r - bi * kTbRows) - 1 - i, ji = j - 1 - i;
+                const bool in = ri >= 0 && (ji & ~63) == chunk;
+                const uint32_t mw = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + (in ? ri : 0)];
+                const int32_t ti = ji - (int32_t)(mw & 0x7FFFFFFFu);
+                const uint16_t *rb = reinterpret_cast<const uint16_t *>(z.lds + buf * kTbBufWords);
+                const uint32_t rc = in && (uint32_t)ti < (uint32_t)kW ? (uint32_t)rb[(uint32_t)ri * 128u + (uint32_t)ti] : 0u;
+                const bool ok = in && (uint32_t)ti < (uint32_t)kW && !(mw & 0x80000000u) && (rc & 0x3F3u) == 0x10u;
+                const uint64_t bad = ~ballot(ok);
+                const uint32_t k = (uint32_t)__builtin_ctzll(bad);  // cells r-1 .. r-k continue the run (k < 64)
+                // base b = j - 1 - i gets ALN | (r - 1 - i): lane b & 63 reads lane (j - 1 - b) & 63
+                const uint32_t src = (uint32_t)(j - 1 - (int32_t)(chunk + (int32_t)lane)) & 63u;
+                const uint32_t val = (EV_ALN << 30) | (r - 1 - lane);
+                const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4u), (int)val);
+                const int32_t b = chunk + (int32_t)lane;
+                if (b <= j - 1 && b > j - 1 - (int32_t)k) vev = got;
+                j -= (int32_t)k;
+                r -= k;
             }
-            r = rr, j = jj, st = (int32_t)stt, nev = ne, guard = g;
+            step_j();
+            to_pred(mt, (rec >> 4) & 63u);
+            rec = cell(mt);
+            continue;
         }
-        DP_STAMP(kPfSpare1);
-        r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
-        j = __builtin_amdgcn_readfirstlane(j);
-        st = __builtin_amdgcn_readfirstlane(st);
-        done = __builtin_amdgcn_readfirstlane(done);
-        err = __builtin_amdgcn_readfirstlane(err);
-        guard = (uint32_t)__builtin_amdgcn_readfirstlane((int)guard);
-        nev = (uint32_t)__builtin_amdgcn_readfirstlane((int)nev);
-        lead_row = (uint32_t)__builtin_amdgcn_readfirstlane((int)lead_row);
-        lead_j = (uint32_t)__builtin_amdgcn_readfirstlane((int)lead_j);
-        far_pred = (uint32_t)__builtin_amdgcn_readfirstlane((int)far_pred);
-        if (far_pred != kNone) r = uni(pred[far_pred]);  // the step's predecessor, slot >= 4
-        wsync();
-        for (uint32_t i = lane; i < nev; i += 64) ev[jhi - (int32_t)i] = evs[i];
-        wsync();
-        DP_STAMP(kPfFlush);
+        if (hc == HC_MSRC) {
+            emit((EV_ALN << 30) | r);
+            lead_row = r;
+            lead_j = (uint32_t)j;
+            break;
+        }
+        if (hc == HC_DEL) {
+            // state D: follow D tags while the cell's D extends its predecessor's D
+            for (;;) {
+                const uint32_t ext = rec & 4u;
+                to_pred(mt, (rec >> 10) & 63u);
+                rec = cell(mt);
+                if (!ext || ++guard > glim) break;
+            }
+            continue;
+        }
+        // state I: insertions along the row
+        for (;;) {
+            emit((EV_INS << 30) | r);
+            const uint32_t ext = rec & 8u;
+            step_j();
+            rec = cell(mt);
+            if (!ext || ++guard > glim) break;
+        }
     }
     if (err) {
         z.status = err;
+        wsync();
         return;
     }
+    // the chunk in flight, then LEAD for every base before the MSRC cell
+    if ((int32_t)lane + chunk >= (int32_t)lead_j && lane <= top) ev[chunk + (int32_t)lane] = vev;
     for (uint32_t jj = lane; jj < lead_j; jj += 64) ev[jj] = (EV_LEAD << 30) | lead_row;
     wsync();
 }
@@ -1771,25 +1383,23 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
     // {base | chain << 3 | np << 8, p0, p1, p2} + p3 (dp_fast's prefetch)
     uint4 *rrec = P<uint4>(z, z.L.rrec);
     uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
-    uint32_t slow = 0;
     for (uint32_t x = lane; x < R; x += 64) {
         const uint32_t n = x + shift[x];
         uint32_t o = poff2[n];
         const uint32_t e0 = poff[x], e1 = poff[x + 1];
         const uint32_t ad = addp[n];
         const uint32_t np = e1 - e0 + (ad != kNone ? 1u : 0u);
-        slow |= np > 4u;
         uint32_t ps[4] = {0, 0, 0, 0}, s = 0;
         for (uint32_t e = e0; e < e1; ++e, ++s) {
             const uint32_t p = pred[e] + shift[pred[e]];
             pred2[o++] = p;
             if (s < 4) ps[s] = p;
-            if (n - p > (uint32_t)kRing) spf[p] = 1, slow = 1;
+            if (n - p > (uint32_t)kRing) spf[p] = 1;
         }
         if (ad != kNone) {
             pred2[o] = ad;
             if (s < 4) ps[s] = ad;
-            if (n - ad > (uint32_t)kRing) spf[ad] = 1, slow = 1;
+            if (n - ad > (uint32_t)kRing) spf[ad] = 1;
         }
         const uint32_t chain = (np == 1 && ps[0] + 1 == n) ? kInfoChain : 0u;
         uint32_t far = np > 4u ? kInfoFar : 0u;
@@ -1804,13 +1414,12 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         uint32_t info = (uint32_t)iinf[i] & 3u;
         if (ad != kNone) {
             pred2[poff2[n]] = ad;
-            if (n - ad > (uint32_t)kRing) spf[ad] = 1, slow = 1;
+            if (n - ad > (uint32_t)kRing) spf[ad] = 1;
             info |= (1u << 8) | (ad + 1 == n ? kInfoChain : 0u) | (n - ad > (uint32_t)kRing ? kInfoFar : 0u);
         }
         rrec[n] = make_uint4(info, ad != kNone ? ad : 0u, 0u, 0u);
         rp3[n] = 0;
     }
-    z.slow = ballot(slow != 0) != 0;
     // M5: first/last rows of the reads
     uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
     for (uint32_t kk = lane; kk < k; kk += 64)
@@ -2040,13 +1649,11 @@ __global__ void __launch_bounds__(128, 2) ccsx_zmw_kernel(KArgs a)
     z.ws = a.ws + z.d.ws_off;
     z.seq = a.seq + z.d.seq_off;
     z.lds = smem;
-    z.meta = smem + kLdsMeta;
     z.rd = reinterpret_cast<uint8_t *>(smem + kLdsFixed);
     z.pos = reinterpret_cast<uint32_t *>(smem + kLdsFixed) + a.lds_read_words;
     z.rdcap = (a.lds_read_words - 2) * 8;
     z.status = kOk;
     z.cells = 0;
-    z.slow = 0;
 #pragma unroll
     for (int i = 0; i < kProfSlots; ++i) z.pf[i] = 0;
     if (threadIdx.x >= 64) {

@@ -24,17 +24,17 @@ constexpr int kRingA = 20;     // its ring rows: kRing predecessor rows + 2 bloc
 constexpr int kPubSlots = 4;   // rows of {M0, M1, insertion prefix} handed from wave 0 to wave 1
 constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-// fixed LDS words per wave: DP ring + ring meta + flush staging (codes, meta,
-// slots); the packed read and the shredding cursors follow (ccsx_kernel.hip)
-constexpr int kLdsFixedWords =
-    kRingA * kRowW + kRing * 4 + 16 * 16 + 16 * 2 + 16 * 64 + kPubSlots * 192 + 64 + 16;
+// fixed LDS words per workgroup: DP ring, record staging, wave 0 -> wave 1
+// hand-off, band offsets, job; the read and the shredding cursors follow
+// (ccsx_kernel.hip)
+constexpr int kLdsFixedWords = kRingA * kRowW + 16 * 64 + kPubSlots * 192 + 64 + 16;
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
 enum Status : int32_t {
     kOk = 0,
     kErrRows = 1,      // graph rows exceed rcap
     kErrEdges = 2,     // edges exceed ecap
-    kErrMulti = 3,     // multi-predecessor rows exceed mcap
+    kErrMulti = 3,     // (unused: kept so status values stay stable)
     kErrSpill = 4,     // spilled DP rows exceed scap
     kErrInDegree = 5,  // node in-degree > 255
     kErrReadLen = 6,   // pushed read longer than the LDS read buffer
@@ -51,14 +51,14 @@ struct ZmwDesc {
     uint64_t msa_off;   // byte offset of the MSA output slab (kSinglePoa only)
     uint32_t seg0;      // index of the first segment in the segment arrays
     uint32_t n;         // number of segments (pushed reads)
-    uint32_t rcap, ecap, lcap, mcap, scap, nw;
+    uint32_t rcap, ecap, lcap, scap, nw;
     uint32_t outcap;    // output slab capacity (bytes)
     uint32_t msacap;    // MSA slab capacity (bytes)
 };
 
 struct ZLayout {
     uint64_t nb0, mem0, poff0, pred0, nb1, mem1, poff1, pred1;
-    uint64_t rmeta, spf, sslot, codes, slots, spill, rrec, rp3;
+    uint64_t rmeta, spf, sslot, codes, spill, rrec, rp3;
     uint64_t ev, tgt, ipt, iinf, ifix, cnt, fixf, addp, cntn;
     uint64_t colof, cons, cmask, colrow, rdoff, rdlen, rfirst, rlast, rfc, rlc;
     uint64_t total;
@@ -82,12 +82,11 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
     L.mem1 = take(uint64_t(d.rcap) * d.nw * 8);
     L.poff1 = take(uint64_t(d.rcap + 1) * 4);
     L.pred1 = take(uint64_t(d.ecap) * 4);
-    L.rmeta = take(uint64_t(d.rcap) * 8);              // per DP row: band offset, multi-slot ordinal
+    L.rmeta = take(uint64_t(d.rcap) * 8);              // per DP row: band offset, far flag
     L.spf = take(d.rcap);                              // per row: needed beyond the LDS ring
     L.sslot = take(uint64_t(d.rcap) * 4);              // per spilled row: its spill record
-    L.codes = take(uint64_t(d.rcap) * 64);             // traceback codes, 4 bits/cell, 64 B/row
-    L.slots = take(uint64_t(d.mcap) * 256);            // predecessor slots of multi-predecessor rows
-    L.spill = take(uint64_t(d.scap) * (kW * 8 + 16));  // spilled rows: H/D + off/rmax/rarg
+    L.codes = take(uint64_t(d.rcap) * 256);            // cell records, 16 bits/cell, 256 B/row
+    L.spill = take(uint64_t(d.scap) * (kW * 8 + 16));  // spilled rows: H, D, band offset, row-max key
     L.rrec = take(uint64_t(d.rcap) * 16);              // per row: {info, p0, p1, p2} for the DP prefetch
     L.rp3 = take(uint64_t(d.rcap) * 4);                // per row: 4th predecessor
     L.ev = take(uint64_t(d.lcap) * 4);
@@ -118,7 +117,7 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 // Tight caps (the default launch) size the DP/graph arrays for the graphs a
 // ZMW really builds -- rows ~ window length x (1 + error rate x reads) -- at
 // a fraction of the memory; every cap is checked on the device (kErrRows,
-// kErrEdges, kErrMulti, kErrSpill) and ccsx_gpu_run re-runs a ZMW that hits
+// kErrEdges, kErrSpill) and ccsx_gpu_run re-runs a ZMW that hits
 // one with full caps.  tight_rows overrides the tight row cap (tests).
 CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, bool full = true,
                           uint32_t tight_rows = 0)
@@ -126,7 +125,6 @@ CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, boo
     d.n = n;
     d.rcap = uint32_t(S + 16);
     d.ecap = uint32_t(S + n + 16);
-    d.mcap = d.rcap / 2 + 64;
     d.scap = d.rcap / 4 + 64;
     if (!full) {
         uint64_t r = tight_rows ? tight_rows : 3ull * lmax + 4096;
@@ -134,7 +132,6 @@ CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, boo
             d.rcap = uint32_t(r + 16);
             d.ecap = 2 * d.rcap;
         }
-        d.mcap = d.rcap / 4 + 64;
         d.scap = d.rcap / 32 + 64;
     }
     d.lcap = lmax + 16;
