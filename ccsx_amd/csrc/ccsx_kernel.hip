@@ -662,6 +662,9 @@ template <bool FULL>
 __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim, uint32_t m, const LaneK &c)
 {
     const int lane = lane_id();
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
     const int li = (int)(r & 63u);
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t base = info & 3u;
@@ -669,14 +672,18 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const uint8_t *rdl = z.rd + lane;
     uint32_t qraw = S.qn;
     int32_t off, Mh0, Mh1, Dv0, Dv1;
-    const bool fast = (info & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain && coff - S.pOff == 1;
+    const int32_t sh = coff - S.pOff;
+    const bool fast = (info & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain && (uint32_t)sh <= 1u;
     if (__builtin_expect(fast, 1)) {
-        // the only predecessor is row r-1 and the band moved by one: its
-        // cells are in registers, shifted one lane by DPP
+        // the only predecessor is row r-1 and the band moved by 0 or 1: its
+        // cells are in registers, shifted by DPP and selected by the move
         off = coff;
-        const int32_t hC = wave_shl1(kNegH, S.H0), dC = wave_shl1(kNeg, S.D0);
-        Mh0 = S.H0, Mh1 = S.H1;
-        Dv0 = max(S.H1 + (kO + kE), S.D1 + kE);
+        const bool s1 = sh != 0;
+        const int32_t hL = wave_shr1(kNegH, S.H1), hR = wave_shl1(kNegH, S.H0), dR = wave_shl1(kNeg, S.D0);
+        Mh0 = s1 ? S.H0 : hL;
+        Mh1 = s1 ? S.H1 : S.H0;
+        const int32_t hC = s1 ? hR : S.H1, dB = s1 ? S.D1 : S.D0, dC = s1 ? dR : S.D1;
+        Dv0 = max(Mh1 + (kO + kE), dB + kE);
         Dv1 = max(hC + (kO + kE), dC + kE);
     } else {
         dpA_cold(z, S, r, info, coff, lim, off, Mh0, Mh1, Dv0, Dv1);
@@ -798,6 +805,9 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
                                         const LaneK &c)
 {
     const int lane = lane_id();
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
     const int li = (int)(r & 63u);
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t np = info >> 8;
@@ -818,8 +828,10 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
         A.ms0 = A.ms1 = A.ds0 = A.ds1 = r - p0;
         A.dx0 = A.Dv0 > hB + (kO + kE) ? 4u : 0u;
         A.dx1 = A.Dv1 > hC + (kO + kE) ? 4u : 0u;
+        DP_STAMP(kPfSpare2);
     } else {
         dpB_cold(z, S, r, info, off, vOff, A);
+        DP_STAMP(kPfSpare3);
     }
     const int32_t srcu = c.src0 + kE * off;
     const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
@@ -853,6 +865,7 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1;
     z.lds[kLdsStRec + (r & 15u) * 64 + lane] = (int32_t)(w0 | (w1 << 16));
     S.vFar = (uint32_t)writelane((int)S.vFar, (int)(info & kInfoFar), li);
+    DP_STAMP(kPfFlush);
 }
 
 // wave 1: rows [r0, r0 + kBlkAB), then the 16-row group's flush: cell
@@ -998,6 +1011,9 @@ __device__ __forceinline__ void dp_helper_exit(Z &z)
     const volatile unsigned long long *pf1 = reinterpret_cast<const volatile unsigned long long *>(z.lds + kLdsPub);
     z.pf[kPfBbusy] += pf1[0];
     z.pf[kPfBwait] += pf1[1];
+    z.pf[kPfSpare2] += pf1[2];
+    z.pf[kPfSpare3] += pf1[3];
+    z.pf[kPfFlush] += pf1[4];
 }
 
 __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
@@ -1096,6 +1112,10 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     uint32_t vev = 0;                      // events of bases [chunk, chunk + 64), lane = base & 63
     int32_t chunk = j & ~63;
     uint32_t top = (uint32_t)(j - chunk);  // highest lane of the chunk that is ours (the rest are INS events)
+    // a completed chunk waits for the next block switch, so that a switch's
+    // wait on the prefetch never waits on a freshly issued store
+    uint32_t vpend = 0, pend_top = 0;
+    int32_t pend = -1;
     uint32_t lead_row = 0, lead_j = 0;
     int32_t err = 0;
     uint32_t guard = 0;
@@ -1110,6 +1130,11 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             bi = nb;
             buf ^= 1u;
             vmeta = tb_put(z, nx, buf);
+            if (pend >= 0) {
+                __builtin_amdgcn_raw_buffer_store_b32(vpend, rev, lane <= pend_top ? (uint32_t)(pend + (int32_t)lane) * 4u : ~0u,
+                                                      0, 0);
+                pend = -1;
+            }
             if (bi) tb_fetch(z, bi - 1, nx);
         }
         mt = (uint32_t)__builtin_amdgcn_readlane((int)vmeta, (int)(r - bi * kTbRows));
@@ -1120,8 +1145,10 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     auto emit = [&](uint32_t e) { vev = (uint32_t)writelane((int)vev, (int)e, j & 63); };
     auto step_j = [&]() {
         if ((j & 63) == 0) {
-            __builtin_amdgcn_raw_buffer_store_b32(vev, rev, lane <= top ? (uint32_t)(chunk + (int32_t)lane) * 4u : ~0u,
-                                                  0, 0);
+            if (pend >= 0)
+                __builtin_amdgcn_raw_buffer_store_b32(vpend, rev, lane <= pend_top ? (uint32_t)(pend + (int32_t)lane) * 4u : ~0u,
+                                                      0, 0);
+            vpend = vev, pend = chunk, pend_top = top;
             chunk -= 64;
             top = 63;
         }
@@ -1199,10 +1226,38 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         wsync();
         return;
     }
-    // the chunk in flight, then LEAD for every base before the MSRC cell
+    // the chunks in flight, then LEAD for every base before the MSRC cell
+    if (pend >= 0 && lane <= pend_top) ev[pend + (int32_t)lane] = vpend;
     if ((int32_t)lane + chunk >= (int32_t)lead_j && lane <= top) ev[chunk + (int32_t)lane] = vev;
     for (uint32_t jj = lane; jj < lead_j; jj += 64) ev[jj] = (EV_LEAD << 30) | lead_row;
     wsync();
+}
+
+// In-place prefix sums over n + 1 words of an HBM array by one wave, eight
+// 64-word chunks loaded ahead of each scan step (the carry makes chunks
+// serial; the loads must not be).  EXCL: out[x] = sum of in[0, x) and the
+// total is returned; else out[x] = sum of in[0, x].
+template <bool EXCL>
+__device__ __forceinline__ uint32_t wave_scan_hbm(const uint32_t *in, uint32_t *out, uint32_t n)
+{
+    const uint32_t lane = lane_id();
+    uint32_t carry = 0;
+    for (uint32_t x0 = 0; x0 < n; x0 += 512) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t x = x0 + 64u * u + lane;
+            v[u] = x < n ? in[x] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t x = x0 + 64u * u + lane;
+            const uint32_t inc = (uint32_t)wave_incl_sum((int)v[u]);
+            if (x < n) out[x] = carry + (EXCL ? inc - v[u] : inc);
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+    }
+    return uni(carry);
 }
 
 // ----------------------------------------------------------------------------
@@ -1245,6 +1300,9 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
     uint32_t *cntn = P<uint32_t>(z, z.L.cntn);
     uint8_t *spf = P<uint8_t>(z, z.L.spf);  // spill flags of the new graph (SPEC.md §3)
 
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
     // M1: classify every read base, number the new nodes in read order
     uint32_t K = 0;
     for (uint32_t j0 = 0; j0 < m; j0 += 64) {
@@ -1301,6 +1359,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         z.status = kErrRows;
         return;
     }
+    DP_STAMP(kPfRowA);
     // M2: shift[x] = #new items with point <= x
     for (uint32_t x = lane; x <= R; x += 64) cnt[x] = 0, fixf[x] = 0;
     wsync();
@@ -1309,21 +1368,13 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         if (ifix[i] != kNone) fixf[ifix[i]] = 1;
     }
     wsync();
-    {
-        uint32_t carry = 0;
-        for (uint32_t x0 = 0; x0 <= R; x0 += 64) {
-            const uint32_t x = x0 + lane;
-            const uint32_t v = x <= R ? cnt[x] : 0u;
-            const uint32_t inc = (uint32_t)wave_incl_sum((int)v);
-            if (x <= R) cnt[x] = carry + inc;
-            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        }
-    }
+    wave_scan_hbm<false>(cnt, cnt, R + 1);
     wsync();
     const uint32_t *shift = cnt;
     auto newidx = [&](uint32_t t) -> uint32_t {
         return (t & kNewBit) ? ipt[t & ~kNewBit] + (t & ~kNewBit) : t + shift[t];
     };
+    DP_STAMP(kPfRowB);
     // M3: at most one new in-edge per target of this read (dedup vs existing)
     for (uint32_t x = lane; x < R2; x += 64) addp[x] = kNone;
     wsync();
@@ -1341,6 +1392,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         if (!dup) addp[newidx(d)] = newidx(s);
     }
     wsync();
+    DP_STAMP(kPfRowC);
     // M4: rows of the new graph
     for (uint32_t x = lane; x < R; x += 64) {
         const uint32_t n = x + shift[x];
@@ -1362,16 +1414,8 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         mem2[(size_t)n * nw + (k >> 6)] |= 1ull << (k & 63u);
     }
     {
-        uint32_t carry = 0;
-        for (uint32_t x0 = 0; x0 < R2; x0 += 64) {
-            const uint32_t x = x0 + lane;
-            const uint32_t v = x < R2 ? cntn[x] : 0u;
-            const uint32_t inc = (uint32_t)wave_incl_sum((int)v);
-            if (x < R2) poff2[x] = carry + inc - v;
-            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        }
-        if (lane == 0) poff2[R2] = carry;
-        const uint32_t E2 = uni(carry);
+        const uint32_t E2 = wave_scan_hbm<true>(cntn, poff2, R2);
+        if (lane == 0) poff2[R2] = E2;
         if (E2 > z.d.ecap) {
             z.status = kErrEdges;
             return;
@@ -1385,26 +1429,38 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
     uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
     for (uint32_t x = lane; x < R; x += 64) {
         const uint32_t n = x + shift[x];
-        uint32_t o = poff2[n];
         const uint32_t e0 = poff[x], e1 = poff[x + 1];
         const uint32_t ad = addp[n];
-        const uint32_t np = e1 - e0 + (ad != kNone ? 1u : 0u);
-        uint32_t ps[4] = {0, 0, 0, 0}, s = 0;
-        for (uint32_t e = e0; e < e1; ++e, ++s) {
+        uint32_t o = poff2[n];
+        const uint32_t ne = e1 - e0;
+        const uint32_t np = ne + (ad != kNone ? 1u : 0u);
+        // the first four old predecessors, loaded together, then their shifts
+        uint32_t q[4], ps[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = (uint32_t)u < ne ? pred[e0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = (uint32_t)u < ne ? q[u] + shift[q[u]] : 0u;
+        uint32_t far = np > 4u ? kInfoFar : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if ((uint32_t)u < ne) {
+                pred2[o + u] = q[u];
+                ps[u] = q[u];
+                if (n - q[u] > (uint32_t)kRing) spf[q[u]] = 1, far = kInfoFar;
+            }
+        }
+        for (uint32_t e = e0 + 4; e < e1; ++e) {
             const uint32_t p = pred[e] + shift[pred[e]];
-            pred2[o++] = p;
-            if (s < 4) ps[s] = p;
+            pred2[o + (e - e0)] = p;
             if (n - p > (uint32_t)kRing) spf[p] = 1;
         }
+        o += ne;
         if (ad != kNone) {
             pred2[o] = ad;
-            if (s < 4) ps[s] = ad;
-            if (n - ad > (uint32_t)kRing) spf[ad] = 1;
+            if (ne < 4) ps[ne] = ad;
+            if (n - ad > (uint32_t)kRing) spf[ad] = 1, far = kInfoFar;
         }
         const uint32_t chain = (np == 1 && ps[0] + 1 == n) ? kInfoChain : 0u;
-        uint32_t far = np > 4u ? kInfoFar : 0u;
-        for (uint32_t e = e0; e < e1; ++e) far |= n - (pred[e] + shift[pred[e]]) > (uint32_t)kRing ? kInfoFar : 0u;
-        if (ad != kNone && n - ad > (uint32_t)kRing) far = kInfoFar;
         rrec[n] = make_uint4((nb[x] & 3u) | chain | far | (np << 8), ps[0], ps[1], ps[2]);
         rp3[n] = ps[3];
     }
@@ -1420,6 +1476,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         rrec[n] = make_uint4(info, ad != kNone ? ad : 0u, 0u, 0u);
         rp3[n] = 0;
     }
+        DP_STAMP(kPfRowE);
     // M5: first/last rows of the reads
     uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
     for (uint32_t kk = lane; kk < k; kk += 64)
@@ -1659,7 +1716,9 @@ __global__ void __launch_bounds__(128, 2) ccsx_zmw_kernel(KArgs a)
     if (threadIdx.x >= 64) {
         dp_helper(z);  // wave 1: the second half of every two-wave DP
         volatile unsigned long long *pf1 = reinterpret_cast<volatile unsigned long long *>(z.lds + kLdsPub);
-        if (lane == 0) pf1[0] = z.pf[kPfBbusy], pf1[1] = z.pf[kPfBwait];
+        if (lane == 0)
+            pf1[0] = z.pf[kPfBbusy], pf1[1] = z.pf[kPfBwait], pf1[2] = z.pf[kPfSpare2], pf1[3] = z.pf[kPfSpare3],
+            pf1[4] = z.pf[kPfFlush];
         __syncthreads();
         return;
     }

@@ -23,5 +23,12 @@ out = {"config": vars(a), "kernel_ms": ms, "gcups": cells / ms / 1e6,
        "cycles_per_zmw": tot / a.n, "row_cycles": {k: round(v / max(p["dp_rows"], 1), 1) for k, v in p.items() if k.startswith("row_")}, "tb_share": {k: round(p[k] / tot, 4) for k in ("spare0", "spare1", "flush")}, "dp_cycles_per_row": p["dp"] / max(p["dp_rows"], 1),
        "rows_per_zmw": p["dp_rows"] / a.n,
        "two_wave": {k: round(p[k] / max(p["tw_rows"], 1), 1) for k in ("a_busy", "a_wait", "b_busy", "b_wait")},
-       "tw_rows_frac": round(p["tw_rows"] / max(p["dp_rows"], 1), 4)}
+       "tw_rows_frac": round(p["tw_rows"] / max(p["dp_rows"], 1), 4),
+       "rows": {"a_fast_pred": round(p["row_A_fast"] / max(p["dp_rows"] - p["row_D_nfast"], 1), 1),
+                "a_cold_pred": round(p["row_B_general"] / max(p["row_D_nfast"], 1), 1),
+                "a_common": round(p["row_C_unused"] / max(p["dp_rows"], 1), 1),
+                "a_cold_frac": round(p["row_D_nfast"] / max(p["dp_rows"], 1), 4),
+                "b_fast_pred_per_row": round(p["spare2"] / max(p["dp_rows"], 1), 1),
+                "b_cold_pred_per_row": round(p["spare3"] / max(p["dp_rows"], 1), 1),
+                "b_common": round(p["flush"] / max(p["dp_rows"], 1), 1)}}
 print(json.dumps(out))
