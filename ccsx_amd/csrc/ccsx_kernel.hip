@@ -890,7 +890,7 @@ __device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             f.slot[k] = reinterpret_cast<const uint4 *>(z.lds + kLdsStRec)[(uint32_t)lane + 64u * k];
-        f.meta = make_uint2((uint32_t)vOff, S.vFar);
+        f.meta = make_uint2((uint32_t)vOff | (S.vFar ? 0x80000000u : 0u), 0u);
         const auto rc = brsrc(z.ws + z.L.codes + (size_t)g0 * 256, nrow * 256);
         const auto rm = brsrc(reinterpret_cast<uint2 *>(z.ws + z.L.rmeta) + g0, nrow * 8);
 #pragma unroll
@@ -975,7 +975,7 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m)
             const int32_t tmin = wave_min((int32_t)tsel);
             wsync();
             uint32_t ej = 0;
-            if (!z.status) ej = reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin].x + (uint32_t)tmin;
+            if (!z.status) ej = (reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin].x & 0x7FFFFFFFu) + (uint32_t)tmin;
             volatile DpJob *job = dp_job(z);
             if (lane == 0) job->er = (uint32_t)rmin, job->ej = ej, job->status = z.status;
         }
@@ -1065,36 +1065,19 @@ constexpr uint64_t kTbAct[3] = {tb_table(0, true), tb_table(1, true), tb_table(2
 constexpr uint64_t kTbNext[3] = {tb_table(0, false), tb_table(1, false), tb_table(2, false)};
 static_assert(2 * kTbBufWords + 128 <= kRingA * kRowW, "traceback buffers live in the DP ring area");
 
-struct TbBlock {
-    uint4 v[8];  // this lane's 128 B of a 32-row block of records
-    uint2 mt;    // lane l < 32: rmeta {band offset, far} of the block's row l
-};
-
-__device__ __forceinline__ void tb_fetch(const Z &z, uint32_t bi, TbBlock &x)
+// LDS-DMA of 32-row block bi into buffer buf: records (8 KB) and the row
+// meta words (band offset | far << 31); the data bypass VGPRs, so nothing in
+// the walk waits on them until the block is entered (explicit s_waitcnt)
+__device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
 {
     const uint32_t lane = lane_id();
-    const uint32_t r0 = bi * kTbRows;
-    const uint32_t n = r0 < z.R ? min(z.R - r0, kTbRows) : 0u;
-    const auto rc = brsrc(z.ws + z.L.codes + (size_t)r0 * 256, n * 256);
+    const uint8_t *src = z.ws + z.L.codes + (size_t)bi * kTbRows * 256 + lane * 16u;
+    int32_t *dst = z.lds + buf * kTbBufWords;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const v4u q = __builtin_amdgcn_raw_buffer_load_b128(rc, (lane + 64u * k) * 16u, 0, 0);
-        x.v[k] = make_uint4(q.x, q.y, q.z, q.w);
-    }
-    const auto rm = brsrc(reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta) + r0, n * 8);
-    const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rm, lane * 8u, 0, 0);
-    x.mt = make_uint2(q.x, q.y);
-}
-
-// records to LDS buffer `buf`, the row meta words (offset | far << 31) to its tail
-__device__ __forceinline__ uint32_t tb_put(const Z &z, const TbBlock &x, uint32_t buf)
-{
-    uint4 *d = reinterpret_cast<uint4 *>(z.lds + buf * kTbBufWords);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d[lane_id() + 64u * k] = x.v[k];
-    const uint32_t w = x.mt.x | (x.mt.y ? 0x80000000u : 0u);
-    z.lds[2 * kTbBufWords + buf * 64 + lane_id()] = (int32_t)w;
-    return w;
+    for (int k = 0; k < 8; ++k)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(src + k * 1024), dst + k * 256, 16, 0, 0);
+    const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + 2u * (bi * kTbRows + lane);
+    __builtin_amdgcn_global_load_lds(ms, z.lds + 2 * kTbBufWords + buf * 64, 4, 0, 0);
 }
 
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
@@ -1104,10 +1087,10 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
     uint32_t r = er, bi = er / kTbRows, buf = 0;
     int32_t j = (int32_t)ej;
-    TbBlock nx;
-    tb_fetch(z, bi, nx);
-    uint32_t vmeta = tb_put(z, nx, buf);
-    if (bi) tb_fetch(z, bi - 1, nx);
+    tb_dma(z, bi, buf);
+    __builtin_amdgcn_s_waitcnt(0);
+    uint32_t vmeta = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
+    if (bi) tb_dma(z, bi - 1, buf ^ 1u);
     const auto rev = brsrc(ev, m * 4);
     uint32_t vev = 0;                      // events of bases [chunk, chunk + 64), lane = base & 63
     int32_t chunk = j & ~63;
@@ -1123,19 +1106,35 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     const uint32_t *poff = G_poff(z, z.cur);
     const uint32_t *pred = G_pred(z, z.cur);
     // the record of cell (r, j); moves to r's block first
+#ifdef CCSX_DP_STAMPS
+    unsigned long long t_prev = stamp();
+#endif
     auto cell = [&](uint32_t &mt) -> uint32_t {
         if (r < bi * kTbRows) {
+#ifdef CCSX_DP_STAMPS
+            z.pf[kPfTbNsw] += 1;
+            const unsigned long long ts0 = stamp();
+#endif
             const uint32_t nb = r / kTbRows;
-            if (nb + 1 != bi) tb_fetch(z, nb, nx);
+            if (nb + 1 != bi) {
+                __builtin_amdgcn_s_waitcnt(0);
+                tb_dma(z, nb, buf ^ 1u);  // not the prefetched neighbour
+            }
             bi = nb;
             buf ^= 1u;
-            vmeta = tb_put(z, nx, buf);
+            __builtin_amdgcn_s_waitcnt(0);
+            vmeta = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
             if (pend >= 0) {
                 __builtin_amdgcn_raw_buffer_store_b32(vpend, rev, lane <= pend_top ? (uint32_t)(pend + (int32_t)lane) * 4u : ~0u,
                                                       0, 0);
                 pend = -1;
             }
-            if (bi) tb_fetch(z, bi - 1, nx);
+            if (bi) tb_dma(z, bi - 1, buf ^ 1u);
+#ifdef CCSX_DP_STAMPS
+            const unsigned long long ts1 = stamp();
+            z.pf[kPfTbSwitch] += ts1 - ts0;
+            t_prev += ts1 - ts0;
+#endif
         }
         mt = (uint32_t)__builtin_amdgcn_readlane((int)vmeta, (int)(r - bi * kTbRows));
         const int32_t t = j - (int32_t)(mt & 0x7FFFFFFFu);
@@ -1165,9 +1164,13 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             err = kErrTrace;
             break;
         }
+#ifdef CCSX_DP_STAMPS
+        z.pf[kPfSpare0] += 1;
+#endif
         const uint32_t hc = rec & 3u;
         if (hc == HC_MPRED) {  // state H
             emit((EV_ALN << 30) | r);
+            bool probed = false;
             if ((rec & 0x3F3u) == 0x10u && !(mt & 0x80000000u) && (j & 63) != 0 && r > bi * kTbRows) {
                 // diagonal run: lane i checks that cell (r-1-i, j-1-i) is MPRED to
                 // the row above it, inside this block and this event chunk; the
@@ -1188,12 +1191,20 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4u), (int)val);
                 const int32_t b = chunk + (int32_t)lane;
                 if (b <= j - 1 && b > j - 1 - (int32_t)k) vev = got;
+#ifdef CCSX_DP_STAMPS
+                z.pf[kPfSpare1] += k;
+                z.pf[kPfRowD] += 1;
+#endif
                 j -= (int32_t)k;
                 r -= k;
+                probed = true;
             }
             step_j();
             to_pred(mt, (rec >> 4) & 63u);
             rec = cell(mt);
+            if (probed) DP_STAMP(kPfTbProbe);
+            else DP_STAMP(kPfTbStep);
+            (void)probed;
             continue;
         }
         if (hc == HC_MSRC) {
@@ -1210,6 +1221,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 rec = cell(mt);
                 if (!ext || ++guard > glim) break;
             }
+            DP_STAMP(kPfTbDI);
             continue;
         }
         // state I: insertions along the row
@@ -1220,6 +1232,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             rec = cell(mt);
             if (!ext || ++guard > glim) break;
         }
+        DP_STAMP(kPfTbDI);
     }
     if (err) {
         z.status = err;

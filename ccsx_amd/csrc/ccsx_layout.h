@@ -164,6 +164,9 @@ enum ProfSlot { kPfTotal = 0, kPfLoad, kPfDp, kPfTrace, kPfMerge, kPfColumns, kP
                 kPfRowA, kPfRowB, kPfRowC, kPfRowD, kPfRowE, kPfFlush, kPfSpare0, kPfSpare1,
                 // two-wave DP (diagnostic build): wave 0 / wave 1 busy and barrier-wait
                 // cycles, rows through the two-wave and the single-wave DP
-                kPfAbusy, kPfAwait, kPfBbusy, kPfBwait, kPfTwRows, kPfSwRows, kPfSpare2, kPfSpare3, kProfSlots };
+                kPfAbusy, kPfAwait, kPfBbusy, kPfBwait, kPfTwRows, kPfSwRows, kPfSpare2, kPfSpare3,
+                // traceback (diagnostic build): cycles of probe steps, plain MPRED steps,
+                // D / I runs, block switches; number of block switches
+                kPfTbProbe, kPfTbStep, kPfTbDI, kPfTbSwitch, kPfTbNsw, kPfSpare4, kPfSpare5, kPfSpare6, kProfSlots };
 
 }  // namespace ccsx

@@ -279,7 +279,8 @@ class Engine:
 
     PROF_SLOTS = ("total", "load_read", "dp", "traceback", "merge", "columns", "shred", "dp_rows",
                   "row_A_fast", "row_B_general", "row_C_unused", "row_D_nfast", "row_E_store_loop", "flush", "spare0", "spare1",
-                  "a_busy", "a_wait", "b_busy", "b_wait", "tw_rows", "sw_rows", "spare2", "spare3")
+                  "a_busy", "a_wait", "b_busy", "b_wait", "tw_rows", "sw_rows", "spare2", "spare3",
+                  "tb_probe", "tb_step", "tb_di", "tb_switch", "tb_nsw", "spare4", "spare5", "spare6")
 
     def set_profiling(self, on: bool = True) -> None:
         self._L.ccsx_gpu_set_profiling(self._ctx, 1 if on else 0)

@@ -114,3 +114,20 @@ def test_tight_caps_fail_loudly_without_rerun(engine):
             engine.fetch()
     finally:
         engine.set_tight_rows(0)
+
+
+@pytest.mark.parametrize("L,passes,n,mode", [(1500, 70, 2, cx.MODE_SHRED), (2500, 66, 2, cx.MODE_PRIMITIVE)])
+def test_wide_graphs(engine, L, passes, n, mode):
+    """More than 64 reads (two membership words), in-degrees above 4 and
+    predecessors beyond the DP ring: the far-row path with slot tags and the
+    HBM spill records of the two-wave DP."""
+    zs = [synth(3000 + h, L, passes) for h in range(n)]
+    _check(engine, zs, mode)
+
+
+@pytest.mark.parametrize("L,passes,mode", [(60, 12, cx.MODE_SHRED), (100, 12, cx.MODE_PRIMITIVE), (127, 9, cx.MODE_PRIMITIVE)])
+def test_reads_shorter_than_band(engine, L, passes, mode):
+    """Reads shorter than W = 128: the partial-band DP (cells past the read
+    end invalid, the free end inside the band)."""
+    zs = [synth(4000 + h, L, passes) for h in range(16)]
+    _check(engine, zs, mode)

@@ -31,4 +31,5 @@ out = {"config": vars(a), "kernel_ms": ms, "gcups": cells / ms / 1e6,
                 "b_fast_pred_per_row": round(p["spare2"] / max(p["dp_rows"], 1), 1),
                 "b_cold_pred_per_row": round(p["spare3"] / max(p["dp_rows"], 1), 1),
                 "b_common": round(p["flush"] / max(p["dp_rows"], 1), 1)}}
+out["per_zmw"] = {k: round(v / a.n, 1) for k, v in p.items()}
 print(json.dumps(out))
