@@ -191,6 +191,7 @@ def main():
                          "traffic": load_traffic(args.config),
                          "kernel": "ccsx_zmw_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "ops_per_cell": OPS_PER_CELL},
+            "step_ms": [round(k, 3) for k in kernel_ms],
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(zs, cfg)

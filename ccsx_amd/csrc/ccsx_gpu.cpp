@@ -209,7 +209,9 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     }
     c->seq_bytes = seq_b, c->ws_bytes = ws_b, c->out_bytes = out_b, c->msa_bytes = msa_b;
     c->nseg_total = nseg;
-    c->lds_read_words = (lmax_all + 7) / 8 + 2;  // nibble-pair read buffer (ccsx_kernel.hip load_read)
+    // nibble-pair read buffer (ccsx_kernel.hip load_read); at least one band:
+    // every lane reads its window bytes even when the read is shorter
+    c->lds_read_words = (std::max<uint32_t>(lmax_all, ccsx::kW) + 7) / 8 + 2;
     c->lds_nmax = std::max<uint32_t>(nmax, 1);
     size_t freeb = 0, totb = 0;
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
@@ -456,6 +458,14 @@ int ccsx_gpu_profile(ccsx_ctx *c, uint64_t *sums, uint32_t nslots)
     for (uint32_t i = 0; i < nslots; ++i) sums[i] = 0;
     for (size_t z = 0; z < c->nz; ++z)
         for (int i = 0; i < ccsx::kProfSlots; ++i) sums[i] += c->h_prof[z * ccsx::kProfSlots + i];
+    return 0;
+}
+
+int ccsx_gpu_profile_zmw(ccsx_ctx *c, uint64_t *out, uint32_t nzmw, uint32_t nslots)
+{
+    if (!c || !c->profiling || nslots < (uint32_t)ccsx::kProfSlots || nzmw < c->nz) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->nz) HIPCHK(c, hipMemcpy(out, c->d_prof.p, c->nz * ccsx::kProfSlots * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 

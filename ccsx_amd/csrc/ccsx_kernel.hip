@@ -97,17 +97,17 @@ __device__ __forceinline__ int wave_incl_sum(int v)
     return v;
 }
 
-// lane within the wave; the workgroup is two waves (wave 0 runs every phase,
-// wave 1 is the DP helper, see dp_align)
+// lane within the wave; the workgroup is three waves (wave 0 runs every
+// phase, waves 1 and 2 are the DP helpers, see dp_align)
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // Visibility point for single-wave phases: LDS and global accesses of the
 // wave before it are complete (the workgroup barrier is reserved for the
-// two-wave DP protocol, which both waves must enter the same number of times)
+// DP protocol, which every wave must enter the same number of times)
 __device__ __forceinline__ void wsync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
 
-// Workgroup barrier for the two-wave DP's block handoff: only LDS must be
-// complete (__syncthreads would also drain wave 1's in-flight HBM stores)
+// Workgroup barrier for the DP's block handoff: only LDS must be complete
+// (__syncthreads would also drain the helpers' in-flight HBM stores)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old, v); }  // lane l <- l-1
@@ -117,11 +117,11 @@ __device__ __forceinline__ int wave_shl1(int old, int v) { return dpp<0x130>(old
 // lane `l` of v <- the uniform value x (v_writelane_b32; l and x in SGPRs)
 __device__ __forceinline__ int writelane(int v, int x, int l)
 {
-    // gfx9 VOP3 reads one SGPR: the lane select goes through m0
-    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
+    // gfx9 VOP3 reads one SGPR: the lane select goes through m0, given to the
+    // compiler as an operand so it keeps m0's other uses (LDS DMA) intact
+    asm volatile("v_writelane_b32 %0, %1, %2"
                  : "+v"(v)
-                 : "s"(__builtin_amdgcn_readfirstlane(x)), "s"(__builtin_amdgcn_readfirstlane(l))
-                 : "m0");
+                 : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(__builtin_amdgcn_readfirstlane(l)));
     return v;
 }
 
@@ -247,28 +247,12 @@ __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
 
 // LDS layout of a workgroup (int32 words)
 constexpr int kLdsRing = 0;                              // kRingA DP rows x kRowW (traceback: 2 blocks)
-constexpr int kLdsStRec = kLdsRing + kRingA * kRowW;     // 16 rows x 256 B of cell records (wave 1)
-constexpr int kLdsPub = kLdsStRec + 16 * 64;             // kPubSlots x {M0, M1, Pex} x 64: wave 0 -> wave 1
-constexpr int kLdsOffRing = kLdsPub + kPubSlots * 192;   // 64: band offset of DP row q at q & 63
+constexpr int kLdsPub = kLdsRing + kRingA * kRowW;       // kPubSlots x Pex x 64: wave 0 -> waves 1, 2
+constexpr int kLdsOffRing = kLdsPub + kPubSlots * 64;    // 64: band offset of DP row q at q & 63
 constexpr int kLdsJob = kLdsOffRing + 64;                // 16: two-wave DP job / results
 constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
 static_assert(kLdsFixed == kLdsFixedWords, "host and device LDS layouts disagree");
-
-// Register set of one flush of wave 1.  Two sets alternate (even/odd 16-row
-// groups) and each is pinned live until it is rewritten a group later, so the
-// global stores of a flush never stall the DP on a store-data (WAR) wait.
-struct FlushBuf {
-    uint2 meta;
-    uint4 slot[4];
-};
-
-__device__ __forceinline__ void pin(FlushBuf &f)
-{
-    asm volatile("" : "+v"(f.meta.x), "+v"(f.meta.y));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(f.slot[i].x), "+v"(f.slot[i].y), "+v"(f.slot[i].z), "+v"(f.slot[i].w));
-}
 
 // per lane: row r0+lane's info and first four predecessors
 struct RowPre {
@@ -291,20 +275,21 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
 }
 
 // ----------------------------------------------------------------------------
-// SPEC.md §3 on two waves.  One wave alone issues about one instruction per
+// SPEC.md §3 on three waves.  One wave alone issues about one instruction per
 // 6 clocks whatever else runs on its SIMD (tools/ubench/issue.hip), and a
-// batch of ~1,000 ZMWs puts ~1 wave on each of the 1,024 SIMDs, so the DP of
-// one ZMW is split across the two waves of its workgroup:
+// batch of ~1,000 ZMWs puts ~1 ZMW on each of the 1,024 SIMDs, so the DP of
+// one ZMW is split across the three waves of its workgroup:
 //  * wave 0 ("A") runs the recurrence: band placement, M / D / H', the
 //    insertion prefix-max and row-max scans, H; it writes each row's H and D
 //    to an LDS ring of kRingA rows, the exclusive prefix max (Pex) of the
 //    row's insertion scan and the row's band offset;
-//  * wave 1 ("B") follows one block of kBlkAB rows behind: from the ring it
-//    recomputes every cell's decision bits (SPEC.md §3.2-§3.4: MPRED / MSRC /
+//  * waves 1 and 2 (the helpers) follow one block of kBlkAB = 2 rows behind,
+//    one row each (wave 1 + h takes the rows of parity h): from the ring they
+//    recompute every cell's decision bits (SPEC.md §3.2-§3.4: MPRED / MSRC /
 //    DEL / INS, D-ext, I-ext), the predecessor slots of multi-predecessor
-//    rows and the free-end candidates, stages them and flushes them to HBM.
+//    rows and the free-end candidates, and store the row's records to HBM.
 // The waves meet at one workgroup barrier per block.  Everything else in the
-// kernel runs on wave 0 alone; wave 1 waits in dp_helper for the next DP.
+// kernel runs on wave 0 alone; the helpers wait in dp_helper for the next DP.
 //
 // Value-preserving choices (the oracle is followed bit for bit):
 //  * ring row = [pad4 | H x 128 | pad4][pad4 | D x 128 | pad4]; pads hold
@@ -320,8 +305,11 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
 // ----------------------------------------------------------------------------
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
-constexpr int kBlkAB = 2;  // rows per A/B lockstep block
-static_assert(kPubSlots >= 2 * kBlkAB, "wave 1 reads the block before wave 0's");
+constexpr int kBlkAB = 4;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2
+constexpr int kHelpers = 2;
+constexpr int kBlockThreads = 64 * (1 + kHelpers);
+static_assert(kBlkAB % kHelpers == 0, "each helper takes the same number of rows per block");
+static_assert(kPubSlots >= 2 * kBlkAB, "the helpers read the block before wave 0's");
 static_assert(kRingA >= kRing + 2 * kBlkAB, "B reads predecessors up to kRing rows behind its row");
 
 
@@ -329,10 +317,15 @@ enum JobKind : int32_t { kJobExit = 0, kJobDp = 1 };
 struct DpJob {
     int32_t kind;
     uint32_t m, R, cur;
-    // results (B)
-    uint32_t er, ej;
-    int32_t status;
+    // results of helper wave 1 + h (h = row parity): best free-end value, its
+    // row and read position, status
+    struct {
+        int32_t best;
+        uint32_t er, ej;
+        int32_t status;
+    } res[2];
 };
+static_assert(sizeof(DpJob) <= 16 * 4, "DP job record exceeds its LDS slot");
 
 __device__ __forceinline__ volatile DpJob *dp_job(const Z &z)
 {
@@ -670,75 +663,80 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const uint32_t base = info & 3u;
     const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
     const uint8_t *rdl = z.rd + lane;
-    uint32_t qraw = S.qn;
-    int32_t off, Mh0, Mh1, Dv0, Dv1;
+    const int32_t pb = S.pOff & ~1;  // S.qn: read bytes (pOff >> 1) + lane, + 1
     const int32_t sh = coff - S.pOff;
     const bool fast = (info & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain && (uint32_t)sh <= 1u;
+    // everything after the predecessor terms; instantiated on both sides of
+    // the fast / cold branch so a fast row meets no further branch
+    auto tail = [&](int32_t off, uint32_t qp, int32_t Mh0, int32_t Mh1, int32_t Dv0, int32_t Dv1,
+                    bool cold) __attribute__((always_inline)) {
+        // the next row's read window, a row ahead of its use (its offset lies
+        // in [off, off + 3] on every fast row)
+        S.qn = (uint32_t)rdl[off >> 1] | (uint32_t)rdl[(off >> 1) + 1] << 8;
+        const uint32_t q0 = qp & 3u, q1 = (qp >> 2) & 3u;
+        const int32_t srcu = c.src0 + kE * off;
+        const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
+        const int32_t M0 = max(Mh0, src0) + (q0 == base ? kMs : kXs);
+        const int32_t M1 = max(Mh1, srcu + kE) + (q1 == base ? kMs : kXs);
+        const int32_t hp0 = max(M0, Dv0), hp1 = max(M1, Dv1);
+        const int32_t X0 = hp0 + c.L4;
+        int32_t incl = max(X0, hp1 + c.L4 + 2);
+        int32_t rk0 = (hp0 << 7) | c.kc0, rk1 = (hp1 << 7) | c.kc1;
+        if (!FULL) {
+            if ((uint32_t)c.L2 >= m) rk0 = INT32_MIN, Dv0 = kNeg;
+            if ((uint32_t)c.L2 + 1 >= m) rk1 = INT32_MIN, Dv1 = kNeg;
+        }
+        int32_t rk = max(rk0, rk1);
+        wave_incl_max2(incl, rk);
+        const int32_t Pex = wave_shr1(kNeg, incl);
+        int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(max(Pex, X0) + c.cI1, hp1);
+        if (!FULL) {
+            if ((uint32_t)c.L2 >= m) nH0 = kNegH;
+            if ((uint32_t)c.L2 + 1 >= m) nH1 = kNegH;
+        }
+        const int32_t key = __builtin_amdgcn_readlane(rk, 63);
+        // ring row, Pex for the helpers, meta window
+        int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kHc + c.L2);
+        row[0] = make_int2(nH0, nH1);
+        row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
+        z.lds[kLdsPub + (r % kPubSlots) * 64 + lane] = Pex;
+        S.vOff = writelane(S.vOff, off, li);
+        S.vKey = writelane(S.vKey, key, li);
+        if (cold && (info & kInfoSpill)) {
+            // a successor lies beyond the ring: keep this row in HBM
+            const uint32_t sl = S.nspill++;
+            if (sl < z.d.scap) {
+                int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)sl * kSpillRec);
+                reinterpret_cast<int2 *>(rec)[lane] = make_int2(nH0, nH1);
+                reinterpret_cast<int2 *>(rec + kW)[lane] = make_int2(Dv0, Dv1);
+                if (lane == 0) rec[256] = off, rec[257] = key, P<uint32_t>(z, z.L.sslot)[r] = sl;
+            } else {
+                z.status = kErrSpill;
+            }
+            wsync();  // visible to every wave before any reader (> kRing rows later)
+        }
+        S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
+        S.pOff = off;
+        S.pArg = off + 127 - (key & 127);
+    };
     if (__builtin_expect(fast, 1)) {
         // the only predecessor is row r-1 and the band moved by 0 or 1: its
         // cells are in registers, shifted by DPP and selected by the move
-        off = coff;
         const bool s1 = sh != 0;
         const int32_t hL = wave_shr1(kNegH, S.H1), hR = wave_shl1(kNegH, S.H0), dR = wave_shl1(kNeg, S.D0);
-        Mh0 = s1 ? S.H0 : hL;
-        Mh1 = s1 ? S.H1 : S.H0;
+        const int32_t Mh0 = s1 ? S.H0 : hL;
+        const int32_t Mh1 = s1 ? S.H1 : S.H0;
         const int32_t hC = s1 ? hR : S.H1, dB = s1 ? S.D1 : S.D0, dC = s1 ? dR : S.D1;
-        Dv0 = max(Mh1 + (kO + kE), dB + kE);
-        Dv1 = max(hC + (kO + kE), dC + kE);
+        const int32_t Dv0 = max(Mh1 + (kO + kE), dB + kE);
+        const int32_t Dv1 = max(hC + (kO + kE), dC + kE);
+        tail(coff, S.qn >> (4u * (uint32_t)(coff - pb)), Mh0, Mh1, Dv0, Dv1, false);  // coff - pb in [0, 2]
     } else {
+        int32_t off, Mh0, Mh1, Dv0, Dv1;
         dpA_cold(z, S, r, info, coff, lim, off, Mh0, Mh1, Dv0, Dv1);
-        if (off != coff) qraw = rdl[off >> 1];
+        const uint32_t d = (uint32_t)(off - pb);
+        const uint32_t qp = d <= 3u ? S.qn >> (4u * d) : (uint32_t)rdl[off >> 1] >> ((uint32_t)(off & 1) * 4u);
+        tail(off, qp, Mh0, Mh1, Dv0, Dv1, true);
     }
-    const uint32_t qp = qraw >> ((uint32_t)(off & 1) * 4u);
-    const uint32_t q0 = qp & 3u, q1 = (qp >> 2) & 3u;
-    const int32_t srcu = c.src0 + kE * off;
-    const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
-    const int32_t M0 = max(Mh0, src0) + (q0 == base ? kMs : kXs);
-    const int32_t M1 = max(Mh1, srcu + kE) + (q1 == base ? kMs : kXs);
-    const int32_t hp0 = max(M0, Dv0), hp1 = max(M1, Dv1);
-    const int32_t X0 = hp0 + c.L4;
-    int32_t incl = max(X0, hp1 + c.L4 + 2);
-    int32_t rk0 = (hp0 << 7) | c.kc0, rk1 = (hp1 << 7) | c.kc1;
-    if (!FULL) {
-        if ((uint32_t)c.L2 >= m) rk0 = INT32_MIN, Dv0 = kNeg;
-        if ((uint32_t)c.L2 + 1 >= m) rk1 = INT32_MIN, Dv1 = kNeg;
-    }
-    int32_t rk = max(rk0, rk1);
-    wave_incl_max2(incl, rk);
-    const int32_t Pex = wave_shr1(kNeg, incl);
-    int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(max(Pex, X0) + c.cI1, hp1);
-    if (!FULL) {
-        if ((uint32_t)c.L2 >= m) nH0 = kNegH;
-        if ((uint32_t)c.L2 + 1 >= m) nH1 = kNegH;
-    }
-    const int32_t key = __builtin_amdgcn_readlane(rk, 63);
-    // ring row, {M0, M1, Pex} for wave 1, meta window
-    int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kHc + c.L2);
-    row[0] = make_int2(nH0, nH1);
-    row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
-    int32_t *pub = z.lds + kLdsPub + (r % kPubSlots) * 192 + lane;
-    pub[0] = M0;
-    pub[64] = M1;
-    pub[128] = Pex;
-    S.vOff = writelane(S.vOff, off, li);
-    S.vKey = writelane(S.vKey, key, li);
-    if (!fast && (info & kInfoSpill)) {
-        // a successor lies beyond the ring: keep this row in HBM
-        const uint32_t sl = S.nspill++;
-        if (sl < z.d.scap) {
-            int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)sl * kSpillRec);
-            reinterpret_cast<int2 *>(rec)[lane] = make_int2(nH0, nH1);
-            reinterpret_cast<int2 *>(rec + kW)[lane] = make_int2(Dv0, Dv1);
-            if (lane == 0) rec[256] = off, rec[257] = key, P<uint32_t>(z, z.L.sslot)[r] = sl;
-        } else {
-            z.status = kErrSpill;
-        }
-        wsync();  // visible to both waves before any reader (> kRing rows later)
-    }
-    S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
-    S.pOff = off;
-    S.pArg = off + 127 - (key & 127);
-    S.qn = rdl[min(max(S.pArg + 1 - kW / 2, 0), lim) >> 1];
 }
 
 // wave 0: rows [r0, r0 + kBlkAB)
@@ -750,20 +748,22 @@ __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
     dpA_row<FULL>(z, S, r0, lim, m, c);
-    if (r0 + 1 < z.R) dpA_row<FULL>(z, S, r0 + 1, lim, m, c);
-    z.lds[kLdsOffRing + lane] = S.vOff;  // band offsets of the last 64 rows for wave 1
+#pragma unroll
+    for (uint32_t i = 1; i < (uint32_t)kBlkAB; ++i)
+        if (r0 + i < z.R) dpA_row<FULL>(z, S, r0 + i, lim, m, c);
+    z.lds[kLdsOffRing + lane] = S.vOff;  // band offsets of the last 64 rows for the helpers
     recwin_end(S.W, r0);
 }
 
 struct BState {
     int32_t bE;       // best free-end value of this lane's cells
     uint32_t bKey;    // its row * 2 + cell
-    uint32_t vFar;    // lane (q & 63): row q's cell tags are predecessor slots (kInfoFar rows)
+    int32_t bOff;     // its row's band offset
     RecWin W;
-    FlushBuf fa, fb;
+    __amdgpu_buffer_rsrc_t rc;  // cell records of this DP (R rows x 256 B)
 };
 
-// wave 1: the predecessor terms of a row that does not have exactly one
+// helper wave: the predecessor terms of a row that does not have exactly one
 // in-band predecessor (0 or >= 2 predecessors, or a far band shift)
 __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint32_t info, int32_t off,
                                          int32_t vOff, PredAcc &A)
@@ -796,10 +796,11 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
     }
 }
 
-// wave 1: the decision bits of one row (wave 0 wrote its ring row and
+// helper wave: the decision bits of one row (wave 0 wrote its ring row and
 // {M, Pex}).  Output per cell, 16 bits: code (SPEC.md §3.4) | M tag << 4 |
 // D tag << 10; a tag is the distance to the predecessor the cell's M / D
-// came from (its slot on rows flagged far), staged as one word per lane.
+// came from (its slot on rows flagged far).  The row's 64 words go straight
+// to HBM (256 B, one store).
 template <bool FULL>
 __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m, int32_t lim, int32_t vOff,
                                         const LaneK &c)
@@ -812,8 +813,8 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t np = info >> 8;
     const int32_t off = __builtin_amdgcn_readlane(vOff, li);
-    const int32_t *pub = z.lds + kLdsPub + (r % kPubSlots) * 192 + lane;
-    const int32_t M0 = pub[0], M1 = pub[64], Pex = pub[128];
+    const int32_t Pex = z.lds[kLdsPub + (r % kPubSlots) * 64 + lane];
+    const uint32_t qp = (uint32_t)z.rd[(off >> 1) + lane] >> ((uint32_t)(off & 1) * 4u);
     const int2 Dv = reinterpret_cast<const int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kDc + c.L2)[0];
     PredAcc A;
     A.Dv0 = Dv.x, A.Dv1 = Dv.y;
@@ -836,6 +837,10 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const int32_t srcu = c.src0 + kE * off;
     const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
     const bool mp0 = A.Mh0 >= src0, mp1 = A.Mh1 >= srcu + kE;
+    // M as wave 0 computed it (same predecessor terms, same read codes)
+    const uint32_t base = info & 3u;
+    const int32_t M0 = max(A.Mh0, src0) + ((qp & 3u) == base ? kMs : kXs);
+    const int32_t M1 = max(A.Mh1, srcu + kE) + (((qp >> 2) & 3u) == base ? kMs : kXs);
     const bool d0 = A.Dv0 > M0, d1 = A.Dv1 > M1;
     const int32_t hp0 = max(M0, A.Dv0), hp1 = max(M1, A.Dv1);
     // insertions (SPEC.md §3.4) from wave 0's exclusive prefix max
@@ -861,17 +866,16 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
         if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
         if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
     }
-    if (e0 > S.bE) S.bE = e0, S.bKey = r * 2;
-    if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1;
-    z.lds[kLdsStRec + (r & 15u) * 64 + lane] = (int32_t)(w0 | (w1 << 16));
-    S.vFar = (uint32_t)writelane((int)S.vFar, (int)(info & kInfoFar), li);
+    if (e0 > S.bE) S.bE = e0, S.bKey = r * 2, S.bOff = off;
+    if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1, S.bOff = off;
+    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), S.rc, r * 256u + (uint32_t)lane * 4u, 0, 0);
     DP_STAMP(kPfFlush);
 }
 
-// wave 1: rows [r0, r0 + kBlkAB), then the 16-row group's flush: cell
-// records (256 B/row) and row meta {band offset, far flag}
+// helper wave h: rows r0 + h + 2i of the block [r0, r0 + kBlkAB); wave 1 also
+// writes the row meta words {band offset | far << 31} of each 16-row group
 template <bool FULL>
-__device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t m, FlushBuf &f)
+__device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t m, uint32_t h)
 {
     const int lane = lane_id();
     const uint32_t R = z.R;
@@ -879,32 +883,22 @@ __device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
     const int32_t vOff = z.lds[kLdsOffRing + lane];
-    dpB_row<FULL>(z, S, r0, m, lim, vOff, c);
-    if (r0 + 1 < R) dpB_row<FULL>(z, S, r0 + 1, m, lim, vOff, c);
+#pragma unroll
+    for (uint32_t i = h; i < (uint32_t)kBlkAB; i += kHelpers)
+        if (r0 + i < R) dpB_row<FULL>(z, S, r0 + i, m, lim, vOff, c);
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
-    recwin_end(S.W, r0);
-    if ((r0 & 15u) == 16u - kBlkAB || rend == R) {
-        pin(f);
+    if (h == 0 && ((r0 & 15u) == 16u - kBlkAB || rend == R)) {
         const uint32_t g0 = r0 & ~15u;
-        const uint32_t nrow = z.status ? 0u : rend - g0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            f.slot[k] = reinterpret_cast<const uint4 *>(z.lds + kLdsStRec)[(uint32_t)lane + 64u * k];
-        f.meta = make_uint2((uint32_t)vOff | (S.vFar ? 0x80000000u : 0u), 0u);
-        const auto rc = brsrc(z.ws + z.L.codes + (size_t)g0 * 256, nrow * 256);
-        const auto rm = brsrc(reinterpret_cast<uint2 *>(z.ws + z.L.rmeta) + g0, nrow * 8);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            __builtin_amdgcn_raw_buffer_store_b128(v4u{f.slot[k].x, f.slot[k].y, f.slot[k].z, f.slot[k].w}, rc,
-                                                   ((uint32_t)lane + 64u * k) * 16u, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(v2u{f.meta.x, f.meta.y}, rm, (uint32_t)(lane - (int)(g0 & 63u)) * 8u,
-                                              0, 0);
+        const uint32_t far = (S.W.cur.info & kInfoFar) ? 0x80000000u : 0u;
+        const auto rm = brsrc(reinterpret_cast<uint32_t *>(z.ws + z.L.rmeta) + g0, (rend - g0) * 4);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vOff | far, rm, (uint32_t)(lane - (int)(g0 & 63u)) * 4u, 0, 0);
     }
+    recwin_end(S.W, r0);
 }
 
 __device__ __forceinline__ uint32_t dp_nblk(uint32_t R) { return (R + kBlkAB - 1) / kBlkAB; }
 
-// wave 0's side of a two-wave DP (wave 1 is in dp_helper)
+// wave 0's side of a DP (the helpers are in dp_helper)
 template <bool FULL>
 __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
 {
@@ -920,7 +914,7 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
     AState S;
     S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
     S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0;
-    S.qn = z.rd[lane];
+    S.qn = (uint32_t)z.rd[lane] | (uint32_t)z.rd[lane + 1] << 8;
     S.nspill = 0;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
@@ -934,50 +928,50 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
         lds_barrier();
         DP_STAMP(kPfAwait);
     }
-    er_out = uni(job->er);
-    ej_out = uni(job->ej);
-    const int32_t bst = uni(job->status);
+    // the two helpers' candidates cover disjoint rows: max score, then min row
+    const int32_t b0 = uni(job->res[0].best), b1 = uni(job->res[1].best);
+    const uint32_t r0 = uni(job->res[0].er), r1 = uni(job->res[1].er);
+    const bool second = b1 > b0 || (b1 == b0 && r1 < r0);
+    er_out = second ? r1 : r0;
+    ej_out = second ? uni(job->res[1].ej) : uni(job->res[0].ej);
+    const int32_t s0 = uni(job->res[0].status), s1 = uni(job->res[1].status);
+    const int32_t bst = s0 ? s0 : s1;
     if (bst && !z.status) z.status = bst;
     z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
 }
 
-// wave 1's side of one DP
+// helper wave h's side of one DP
 template <bool FULL>
-__device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m)
+__device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
 {
     const int lane = lane_id();
     BState S;
-    S.bE = INT32_MIN, S.bKey = 0, S.vFar = 0;
+    S.bE = INT32_MIN, S.bKey = 0, S.bOff = 0;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
-    S.fa.meta = S.fb.meta = make_uint2(0, 0);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) S.fa.slot[c] = S.fb.slot[c] = make_uint4(0, 0, 0, 0);
+    S.rc = brsrc(z.ws + z.L.codes, z.R * 256u);
     const uint32_t nblk = dp_nblk(z.R);
 #ifdef CCSX_DP_STAMPS
     unsigned long long t_prev = stamp();
 #endif
     for (uint32_t b = 0; b <= nblk; ++b) {
-        if (b >= 1 && !z.status) {
-            const uint32_t bb = b - 1;
-            if ((bb * kBlkAB >> 4) & 1u) dpB_block<FULL>(z, S, bb * kBlkAB, m, S.fb);
-            else dpB_block<FULL>(z, S, bb * kBlkAB, m, S.fa);
-        }
+        if (b >= 1 && !z.status) dpB_block<FULL>(z, S, (b - 1) * kBlkAB, m, h);
         if (b == nblk) {
-            // results: lexicographic (max score, min row, min j) over the lanes
-            pin(S.fa);
-            pin(S.fb);
+            // this wave's candidate: lexicographic (max score, min row, min j)
             const int32_t best = wave_max(S.bE);
             const uint32_t rsel = S.bE == best ? S.bKey >> 1 : 0x7FFFFFFFu;
             const int32_t rmin = wave_min((int32_t)rsel);
             const bool mine = S.bE == best && (S.bKey >> 1) == (uint32_t)rmin;
-            const uint32_t tsel = mine ? 2u * (uint32_t)lane + (S.bKey & 1u) : 0x7FFFFFFFu;
-            const int32_t tmin = wave_min((int32_t)tsel);
-            wsync();
-            uint32_t ej = 0;
-            if (!z.status) ej = (reinterpret_cast<const uint2 *>(z.ws + z.L.rmeta)[rmin].x & 0x7FFFFFFFu) + (uint32_t)tmin;
+            const int32_t jsel = mine ? S.bOff + 2 * lane + (int32_t)(S.bKey & 1u) : INT32_MAX;
+            const int32_t jmin = wave_min(jsel);
+            wsync();  // records and row meta in HBM before wave 0 reads them
             volatile DpJob *job = dp_job(z);
-            if (lane == 0) job->er = (uint32_t)rmin, job->ej = ej, job->status = z.status;
+            if (lane == 0) {
+                job->res[h].best = best;
+                job->res[h].er = best == INT32_MIN ? 0xFFFFFFFFu : (uint32_t)rmin;
+                job->res[h].ej = (uint32_t)jmin;
+                job->res[h].status = z.status;
+            }
         }
         DP_STAMP(kPfBbusy);
         lds_barrier();
@@ -985,8 +979,8 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m)
     }
 }
 
-// wave 1: serve DP jobs until wave 0 posts kJobExit
-__device__ __forceinline__ void dp_helper(Z &z)
+// helper wave h (1 + h = wave index): serve DP jobs until wave 0 posts kJobExit
+__device__ __forceinline__ void dp_helper(Z &z, uint32_t h)
 {
     for (;;) {
         __syncthreads();  // J: job posted
@@ -997,8 +991,8 @@ __device__ __forceinline__ void dp_helper(Z &z)
         z.cur = uni((int)job->cur);
         z.status = kOk;
         const uint32_t m = uni(job->m);
-        if (m >= (uint32_t)kW) dp_wave_b<true>(z, m);
-        else dp_wave_b<false>(z, m);
+        if (m >= (uint32_t)kW) dp_wave_b<true>(z, m, h);
+        else dp_wave_b<false>(z, m, h);
     }
 }
 
@@ -1006,14 +1000,25 @@ __device__ __forceinline__ void dp_helper_exit(Z &z)
 {
     if (lane_id() == 0) dp_job(z)->kind = kJobExit;
     __syncthreads();
-    // wave 1 hands over its diagnostic counters
+    // the helper waves hand over their diagnostic counters
     __syncthreads();
     const volatile unsigned long long *pf1 = reinterpret_cast<const volatile unsigned long long *>(z.lds + kLdsPub);
-    z.pf[kPfBbusy] += pf1[0];
-    z.pf[kPfBwait] += pf1[1];
-    z.pf[kPfSpare2] += pf1[2];
-    z.pf[kPfSpare3] += pf1[3];
-    z.pf[kPfFlush] += pf1[4];
+    for (int h = 0; h < 2; ++h) {
+        z.pf[kPfBbusy] += pf1[8 * h + 0];
+        z.pf[kPfBwait] += pf1[8 * h + 1];
+        z.pf[kPfSpare2] += pf1[8 * h + 2];
+        z.pf[kPfSpare3] += pf1[8 * h + 3];
+        z.pf[kPfFlush] += pf1[8 * h + 4];
+        z.pf[kPfHw1 + h] = pf1[8 * h + 5];
+    }
+}
+
+// placement of the calling wave: HW_ID (wave, SIMD, CU, SE) | XCC_ID << 32
+__device__ __forceinline__ unsigned long long wave_hw_id()
+{
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    return (unsigned long long)hw | (unsigned long long)xcc << 32;
 }
 
 __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
@@ -1076,7 +1081,7 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(src + k * 1024), dst + k * 256, 16, 0, 0);
-    const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + 2u * (bi * kTbRows + lane);
+    const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + bi * kTbRows + lane;
     __builtin_amdgcn_global_load_lds(ms, z.lds + 2 * kTbBufWords + buf * 64, 4, 0, 0);
 }
 
@@ -1705,7 +1710,15 @@ __device__ __forceinline__ void write_msa(Z &z, uint32_t ncols, uint32_t n, uint
     wsync();
 }
 
-__global__ void __launch_bounds__(128, 2) ccsx_zmw_kernel(KArgs a)
+// Occupancy: ~1,000 ZMWs = 1,000 three-wave workgroups on 256 CUs, 4 per CU.
+// At 3 waves per SIMD those fill every wave slot, and the dispatcher then
+// strands some workgroups until others finish (bimodal launch times); 4 waves
+// per SIMD (<= 128 VGPRs) leaves slack.
+#ifndef CCSX_WAVES_PER_EU
+#define CCSX_WAVES_PER_EU 4
+#endif
+__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(CCSX_WAVES_PER_EU)))
+ccsx_zmw_kernel(KArgs a)
 {
     extern __shared__ int32_t smem[];
     if (blockIdx.x >= a.nzmw) return;
@@ -1727,15 +1740,19 @@ __global__ void __launch_bounds__(128, 2) ccsx_zmw_kernel(KArgs a)
 #pragma unroll
     for (int i = 0; i < kProfSlots; ++i) z.pf[i] = 0;
     if (threadIdx.x >= 64) {
-        dp_helper(z);  // wave 1: the second half of every two-wave DP
-        volatile unsigned long long *pf1 = reinterpret_cast<volatile unsigned long long *>(z.lds + kLdsPub);
+        // waves 1 and 2: the decision bits of the even / odd rows of every DP
+        const uint32_t h = uni(threadIdx.x >> 6) - 1u;
+        dp_helper(z, h);
+        volatile unsigned long long *pf1 = reinterpret_cast<volatile unsigned long long *>(z.lds + kLdsPub) + 8 * h;
         if (lane == 0)
             pf1[0] = z.pf[kPfBbusy], pf1[1] = z.pf[kPfBwait], pf1[2] = z.pf[kPfSpare2], pf1[3] = z.pf[kPfSpare3],
-            pf1[4] = z.pf[kPfFlush];
+            pf1[4] = z.pf[kPfFlush], pf1[5] = wave_hw_id();
         __syncthreads();
         return;
     }
     const unsigned long long t_start = stamp();
+    z.pf[kPfStartRt] = __builtin_amdgcn_s_memrealtime();
+    z.pf[kPfHw0] = wave_hw_id();
     const uint32_t n = z.d.n;
     const uint32_t *soff = a.soff + z.d.seg0, *slen = a.slen + z.d.seg0;
     uint32_t *rdoff = P<uint32_t>(z, z.L.rdoff), *rdlen = P<uint32_t>(z, z.L.rdlen);
@@ -1800,6 +1817,7 @@ __global__ void __launch_bounds__(128, 2) ccsx_zmw_kernel(KArgs a)
         a.cells[zi] = z.cells;
         if (a.prof) {
             z.pf[kPfTotal] = stamp() - t_start;
+            z.pf[kPfEndRt] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
             for (int i = 0; i < kProfSlots; ++i) a.prof[(size_t)zi * kProfSlots + i] = z.pf[i];
         }
@@ -1815,6 +1833,6 @@ extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, 
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(128), lds_bytes, s, *a);
+    hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(ccsx::kBlockThreads), lds_bytes, s, *a);
     return hipGetLastError();
 }

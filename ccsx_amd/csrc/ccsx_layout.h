@@ -20,14 +20,13 @@ namespace ccsx {
 constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
 constexpr int kRing = 16;      // DP rows kept in LDS per wave
 constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H and D, each [4 pad | 128 | 4 pad]
-constexpr int kRingA = 20;     // its ring rows: kRing predecessor rows + 2 blocks of wave 1's lag
-constexpr int kPubSlots = 4;   // rows of {M0, M1, insertion prefix} handed from wave 0 to wave 1
+constexpr int kRingA = 24;     // its ring rows: kRing predecessor rows + 2 blocks of the helpers' lag
+constexpr int kPubSlots = 8;   // rows of the insertion prefix max handed from wave 0 to the helpers
 constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-// fixed LDS words per workgroup: DP ring, record staging, wave 0 -> wave 1
-// hand-off, band offsets, job; the read and the shredding cursors follow
-// (ccsx_kernel.hip)
-constexpr int kLdsFixedWords = kRingA * kRowW + 16 * 64 + kPubSlots * 192 + 64 + 16;
+// fixed LDS words per workgroup: DP ring, wave 0 -> waves 1/2 hand-off, band
+// offsets, job; the read and the shredding cursors follow (ccsx_kernel.hip)
+constexpr int kLdsFixedWords = kRingA * kRowW + kPubSlots * 64 + 64 + 16;
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
 enum Status : int32_t {
@@ -82,7 +81,7 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
     L.mem1 = take(uint64_t(d.rcap) * d.nw * 8);
     L.poff1 = take(uint64_t(d.rcap + 1) * 4);
     L.pred1 = take(uint64_t(d.ecap) * 4);
-    L.rmeta = take(uint64_t(d.rcap) * 8);              // per DP row: band offset, far flag
+    L.rmeta = take(uint64_t(d.rcap) * 4);              // per DP row: band offset | far flag << 31
     L.spf = take(d.rcap);                              // per row: needed beyond the LDS ring
     L.sslot = take(uint64_t(d.rcap) * 4);              // per spilled row: its spill record
     L.codes = take(uint64_t(d.rcap) * 256);            // cell records, 16 bits/cell, 256 B/row
@@ -167,6 +166,9 @@ enum ProfSlot { kPfTotal = 0, kPfLoad, kPfDp, kPfTrace, kPfMerge, kPfColumns, kP
                 kPfAbusy, kPfAwait, kPfBbusy, kPfBwait, kPfTwRows, kPfSwRows, kPfSpare2, kPfSpare3,
                 // traceback (diagnostic build): cycles of probe steps, plain MPRED steps,
                 // D / I runs, block switches; number of block switches
-                kPfTbProbe, kPfTbStep, kPfTbDI, kPfTbSwitch, kPfTbNsw, kPfSpare4, kPfSpare5, kPfSpare6, kProfSlots };
+                kPfTbProbe, kPfTbStep, kPfTbDI, kPfTbSwitch, kPfTbNsw,
+                // placement: HW_ID | XCC_ID << 32 of waves 0, 1, 2; start / end on
+                // the constant-rate s_memrealtime clock
+                kPfHw0, kPfHw1, kPfHw2, kPfStartRt, kPfEndRt, kProfSlots };
 
 }  // namespace ccsx

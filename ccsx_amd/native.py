@@ -23,7 +23,7 @@ MODE_PRIMITIVE = 1
 EXPORTS = {
     "ccsx_gpu.h": ["ccsx_gpu_device_count", "ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
-                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_set_tight_rows"],
+                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw"],
     "ccsx_seqio.h": ["ccsx_reader_open", "ccsx_reader_next", "ccsx_reader_close"],
@@ -66,6 +66,8 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_staged_bytes.restype = C.c_uint64
         L.ccsx_gpu_set_profiling.argtypes = [C.c_void_p, C.c_int]
         L.ccsx_gpu_profile.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]
+        if hasattr(L, "ccsx_gpu_profile_zmw"):  # diagnostics; absent from older builds used in A/B runs
+            L.ccsx_gpu_profile_zmw.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32]
         L.ccsx_gpu_set_tight_rows.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_revcomp.argtypes = [C.c_char_p, C.c_uint32]
         L.ccsx_prepare.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
@@ -280,7 +282,7 @@ class Engine:
     PROF_SLOTS = ("total", "load_read", "dp", "traceback", "merge", "columns", "shred", "dp_rows",
                   "row_A_fast", "row_B_general", "row_C_unused", "row_D_nfast", "row_E_store_loop", "flush", "spare0", "spare1",
                   "a_busy", "a_wait", "b_busy", "b_wait", "tw_rows", "sw_rows", "spare2", "spare3",
-                  "tb_probe", "tb_step", "tb_di", "tb_switch", "tb_nsw", "spare4", "spare5", "spare6")
+                  "tb_probe", "tb_step", "tb_di", "tb_switch", "tb_nsw", "hw0", "hw1", "hw2", "start_rt", "end_rt")
 
     def set_profiling(self, on: bool = True) -> None:
         self._L.ccsx_gpu_set_profiling(self._ctx, 1 if on else 0)
@@ -291,6 +293,14 @@ class Engine:
         if self._L.ccsx_gpu_profile(self._ctx, buf, len(self.PROF_SLOTS)) != 0:
             self._err("ccsx_gpu_profile")
         return {k: int(buf[i]) for i, k in enumerate(self.PROF_SLOTS)}
+
+    def profile_zmw(self, nzmw: int) -> list:
+        """The same counters per ZMW of the last launch (staging order)."""
+        ns = len(self.PROF_SLOTS)
+        buf = (C.c_uint64 * (nzmw * ns))()
+        if self._L.ccsx_gpu_profile_zmw(self._ctx, buf, nzmw, ns) != 0:
+            self._err("ccsx_gpu_profile_zmw")
+        return [{k: int(buf[z * ns + i]) for i, k in enumerate(self.PROF_SLOTS)} for z in range(nzmw)]
 
     def staged_bytes(self) -> int:
         return int(self._L.ccsx_gpu_staged_bytes(self._ctx))

@@ -81,6 +81,9 @@ int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
 /* Test hook: tight row capacity override (0 = default 3 x longest segment + 4096). */
 int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
 int ccsx_gpu_profile(ccsx_ctx *ctx, uint64_t *sums, uint32_t nslots);
+/* Diagnostics: the same counters per ZMW (staging order), nslots per ZMW;
+ * out holds nzmw * nslots values. */
+int ccsx_gpu_profile_zmw(ccsx_ctx *ctx, uint64_t *out, uint32_t nzmw, uint32_t nslots);
 
 #ifdef __cplusplus
 }
