@@ -313,10 +313,12 @@ static_assert(kPubSlots >= 2 * kBlkAB, "the helpers read the block before wave 0
 static_assert(kRingA >= kRing + 2 * kBlkAB, "B reads predecessors up to kRing rows behind its row");
 
 
-enum JobKind : int32_t { kJobExit = 0, kJobDp = 1 };
+enum JobKind : int32_t { kJobExit = 0, kJobDp = 1, kJobMerge = 2 };
 struct DpJob {
     int32_t kind;
     uint32_t m, R, cur;
+    uint32_t k;     // merge: read index
+    uint32_t K, E;  // merge: new rows (wave 0's M1), edges of the new graph
     // results of helper wave 1 + h (h = row parity): best free-end value, its
     // row and read position, status
     struct {
@@ -979,7 +981,10 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
     }
 }
 
-// helper wave h (1 + h = wave index): serve DP jobs until wave 0 posts kJobExit
+__device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid);
+
+// helper wave h (1 + h = wave index): serve DP and merge jobs until wave 0
+// posts kJobExit
 __device__ __forceinline__ void dp_helper(Z &z, uint32_t h)
 {
     for (;;) {
@@ -991,7 +996,8 @@ __device__ __forceinline__ void dp_helper(Z &z, uint32_t h)
         z.cur = uni((int)job->cur);
         z.status = kOk;
         const uint32_t m = uni(job->m);
-        if (m >= (uint32_t)kW) dp_wave_b<true>(z, m, h);
+        if (kind == kJobMerge) merge(z, uni(job->k), m, threadIdx.x);
+        else if (m >= (uint32_t)kW) dp_wave_b<true>(z, m, h);
         else dp_wave_b<false>(z, m, h);
     }
 }
@@ -1294,9 +1300,17 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
     return v;
 }
 
-__device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
+// All three waves of the workgroup run the merge (thread tid of kBlockThreads):
+// the row-parallel loops stride over every thread, the phases meet at
+// workgroup barriers (which also make the HBM writes visible); M1's ordered
+// compaction and the two prefix scans run on wave 0 between barriers.  Every
+// branch that skips a barrier is uniform over the workgroup.
+__device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid)
 {
+    constexpr uint32_t T = kBlockThreads;
     const uint32_t lane = lane_id();
+    const bool w0 = tid < 64;
+    volatile DpJob *job = dp_job(z);
     const uint32_t R = z.R, nw = z.d.nw;
     const int a = z.cur, b = a ^ 1;
     const uint8_t *nb = G_nb(z, a);
@@ -1321,9 +1335,9 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
 #ifdef CCSX_DP_STAMPS
     unsigned long long t_prev = stamp();
 #endif
-    // M1: classify every read base, number the new nodes in read order
+    // M1 (wave 0): classify every read base, number the new nodes in read order
     uint32_t K = 0;
-    for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+    for (uint32_t j0 = 0; w0 && j0 < m; j0 += 64) {
         const uint32_t j = j0 + lane;
         bool isnew = false;
         uint32_t pt = 0, cs = 1, fix = kNone, t = 0, bq = 0;
@@ -1372,6 +1386,9 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         }
         K += (uint32_t)__builtin_popcountll(bal);
     }
+    if (w0 && lane == 0) job->K = K;
+    __syncthreads();
+    K = uni(job->K);
     const uint32_t R2 = R + K;
     if (R2 > z.d.rcap) {
         z.status = kErrRows;
@@ -1379,24 +1396,24 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
     }
     DP_STAMP(kPfRowA);
     // M2: shift[x] = #new items with point <= x
-    for (uint32_t x = lane; x <= R; x += 64) cnt[x] = 0, fixf[x] = 0;
-    wsync();
-    for (uint32_t i = lane; i < K; i += 64) {
+    for (uint32_t x = tid; x <= R; x += T) cnt[x] = 0, fixf[x] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < K; i += T) {
         atomicAdd(&cnt[ipt[i]], 1u);
         if (ifix[i] != kNone) fixf[ifix[i]] = 1;
     }
-    wsync();
-    wave_scan_hbm<false>(cnt, cnt, R + 1);
-    wsync();
+    __syncthreads();
+    if (w0) wave_scan_hbm<false>(cnt, cnt, R + 1);
+    __syncthreads();
     const uint32_t *shift = cnt;
     auto newidx = [&](uint32_t t) -> uint32_t {
         return (t & kNewBit) ? ipt[t & ~kNewBit] + (t & ~kNewBit) : t + shift[t];
     };
     DP_STAMP(kPfRowB);
     // M3: at most one new in-edge per target of this read (dedup vs existing)
-    for (uint32_t x = lane; x < R2; x += 64) addp[x] = kNone;
-    wsync();
-    for (uint32_t j = 1 + lane; j < m; j += 64) {
+    for (uint32_t x = tid; x < R2; x += T) addp[x] = kNone;
+    __syncthreads();
+    for (uint32_t j = 1 + tid; j < m; j += T) {
         const uint32_t s = tgt[j - 1], d = tgt[j];
         bool dup = false;
         if (!(d & kNewBit) && !(s & kNewBit)) {
@@ -1409,43 +1426,47 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         }
         if (!dup) addp[newidx(d)] = newidx(s);
     }
-    wsync();
+    __syncthreads();
     DP_STAMP(kPfRowC);
     // M4: rows of the new graph
-    for (uint32_t x = lane; x < R; x += 64) {
+    for (uint32_t x = tid; x < R; x += T) {
         const uint32_t n = x + shift[x];
         nb2[n] = fixf[x] ? (uint8_t)(nb[x] & 3u) : nb[x];
         spf[n] = 0;
         for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = mem[(size_t)x * nw + w];
         cntn[n] = poff[x + 1] - poff[x] + (addp[n] != kNone ? 1u : 0u);
     }
-    for (uint32_t i = lane; i < K; i += 64) {
+    for (uint32_t i = tid; i < K; i += T) {
         const uint32_t n = ipt[i] + i;
         nb2[n] = iinf[i];
         spf[n] = 0;
         for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = 0;
         cntn[n] = addp[n] != kNone ? 1u : 0u;
     }
-    wsync();
-    for (uint32_t j = lane; j < m; j += 64) {
+    __syncthreads();
+    // (one target row per read base, so the read-modify-writes never collide)
+    for (uint32_t j = tid; j < m; j += T) {
         const uint32_t n = newidx(tgt[j]);
         mem2[(size_t)n * nw + (k >> 6)] |= 1ull << (k & 63u);
     }
-    {
+    if (w0) {
         const uint32_t E2 = wave_scan_hbm<true>(cntn, poff2, R2);
-        if (lane == 0) poff2[R2] = E2;
+        if (lane == 0) poff2[R2] = E2, job->E = E2;
+    }
+    __syncthreads();
+    {
+        const uint32_t E2 = uni(job->E);
         if (E2 > z.d.ecap) {
             z.status = kErrEdges;
             return;
         }
         z.E = E2;
     }
-    wsync();
     // predecessor lists of the new graph, and each row's DP record
     // {base | chain << 3 | np << 8, p0, p1, p2} + p3 (dp_fast's prefetch)
     uint4 *rrec = P<uint4>(z, z.L.rrec);
     uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
-    for (uint32_t x = lane; x < R; x += 64) {
+    for (uint32_t x = tid; x < R; x += T) {
         const uint32_t n = x + shift[x];
         const uint32_t e0 = poff[x], e1 = poff[x + 1];
         const uint32_t ad = addp[n];
@@ -1482,7 +1503,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         rrec[n] = make_uint4((nb[x] & 3u) | chain | far | (np << 8), ps[0], ps[1], ps[2]);
         rp3[n] = ps[3];
     }
-    for (uint32_t i = lane; i < K; i += 64) {
+    for (uint32_t i = tid; i < K; i += T) {
         const uint32_t n = ipt[i] + i;
         const uint32_t ad = addp[n];
         uint32_t info = (uint32_t)iinf[i] & 3u;
@@ -1497,18 +1518,18 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m)
         DP_STAMP(kPfRowE);
     // M5: first/last rows of the reads
     uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
-    for (uint32_t kk = lane; kk < k; kk += 64)
+    for (uint32_t kk = tid; kk < k; kk += T)
         if (rfirst[kk] != kNone) {
             rfirst[kk] += shift[rfirst[kk]];
             rlast[kk] += shift[rlast[kk]];
         }
-    if (lane == 0) {
+    if (tid == 0) {
         rfirst[k] = newidx(tgt[0]);
         rlast[k] = newidx(tgt[m - 1]);
     }
     z.R = R2;
     z.cur = b;
-    wsync();
+    __syncthreads();
 }
 
 // ----------------------------------------------------------------------------
@@ -1605,7 +1626,12 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             t1 = stamp();
             z.pf[kPfTrace] += t1 - t2;
         }
-        merge(z, k, m);
+        {
+            volatile DpJob *job = dp_job(z);
+            if (lane_id() == 0) job->kind = kJobMerge, job->m = m, job->R = z.R, job->cur = (uint32_t)z.cur, job->k = k;
+            __syncthreads();  // J: job posted
+            merge(z, k, m, threadIdx.x);
+        }
         if (z.status) return 0;
         z.pf[kPfMerge] += stamp() - t1;
     }
