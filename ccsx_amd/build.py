@@ -98,7 +98,10 @@ def build_product(verbose: bool = False) -> str:
     diag = os.path.join(HERE, "libccsx_amd_diag.so")
     dobj = os.path.join(OBJ, "ccsx_kernel_diag.hip.o")
     if _stale(dobj, [srcs[0]] + hdrs):
-        _run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS"] + common + ["-c", srcs[0], "-o", dobj])
+        # the stamps' counters need registers: 2 waves per SIMD (occupancy is
+        # not what this build measures; per-ZMW cycle counts are)
+        _run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2"] + common
+             + ["-c", srcs[0], "-o", dobj])
     if _stale(diag, objs[1:] + [dobj]):
         _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", diag, dobj] + objs[1:] + ["-lz", "-lpthread"])
     # the C host program

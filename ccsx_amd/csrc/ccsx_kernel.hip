@@ -199,6 +199,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t 
         z.pf[slot] += t_ - t_prev;                                                          \
         t_prev = t_;                                                                        \
     } while (0)
+// a shader-clock read whose result is only waited for later (ROW_STAMPS_END)
+#define ROW_STAMP(var)                                      \
+    do {                                                    \
+        __builtin_amdgcn_sched_barrier(0);                  \
+        asm volatile("s_memtime %0" : "=s"(var)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                  \
+    } while (0)
 #else
 #define DP_STAMP(slot) \
     do {               \
@@ -247,8 +254,8 @@ __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
 
 // LDS layout of a workgroup (int32 words)
 constexpr int kLdsRing = 0;                              // kRingA DP rows x kRowW (traceback: 2 blocks)
-constexpr int kLdsPub = kLdsRing + kRingA * kRowW;       // kPubSlots x Pex x 64: wave 0 -> waves 1, 2
-constexpr int kLdsOffRing = kLdsPub + kPubSlots * 64;    // 64: band offset of DP row q at q & 63
+constexpr int kLdsDiag = kLdsRing + kRingA * kRowW;      // 32: helpers' diagnostic counters at exit
+constexpr int kLdsOffRing = kLdsDiag + 32;               // 64: band offset of DP row q at q & 63
 constexpr int kLdsJob = kLdsOffRing + 64;                // 16: two-wave DP job / results
 constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
@@ -309,7 +316,6 @@ constexpr int kBlkAB = 4;  // rows per lockstep block: helper h takes rows r0 + 
 constexpr int kHelpers = 2;
 constexpr int kBlockThreads = 64 * (1 + kHelpers);
 static_assert(kBlkAB % kHelpers == 0, "each helper takes the same number of rows per block");
-static_assert(kPubSlots >= 2 * kBlkAB, "the helpers read the block before wave 0's");
 static_assert(kRingA >= kRing + 2 * kBlkAB, "B reads predecessors up to kRing rows behind its row");
 
 
@@ -560,6 +566,7 @@ struct AState {
     int32_t vOff, vKey;      // lane (q & 63): band offset / row-max key of row q
     uint32_t qn;             // read codes at the next row's chain offset (loaded a row ahead)
     uint32_t nspill;         // spill records written
+    uint64_t fmask;          // bit q & 63: row q is a chain row without far / spill flags
     RecWin W;
 };
 
@@ -582,7 +589,7 @@ __device__ __forceinline__ LaneK lane_consts(int lane)
 // by 0 or 2 (DPP) and general rows (predecessors from the ring)
 __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r, uint32_t info, int32_t coff,
                                          int32_t lim, int32_t &off_o, int32_t &Mh0, int32_t &Mh1, int32_t &Dv0,
-                                         int32_t &Dv1)
+                                         int32_t &Dv1, int &kind)
 {
     const int lane = lane_id();
     const int li = (int)(r & 63u);
@@ -591,9 +598,12 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
     const int32_t *ring = z.lds + kLdsRing;
     PredAcc A;
     int32_t off;
+    kind = 4;
     if (info & kInfoFar) {
+        kind = 0;
         far_terms<false>(z, r, np, S.vOff, S.vKey, lim, true, off, A);
     } else if ((info & kInfoChain) && (uint32_t)sh <= 2u) {
+        kind = 1;
         // chain row, band moved by 0..2 (1: a spill row)
         off = coff;
         int32_t hA, hB, hC, dB, dC;
@@ -607,12 +617,14 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
         }
         pred_fold<false>(A, 0, 0, hA, hB, hC, dB, dC);
     } else if (np == 1) {
+        kind = 2;
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
         const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
         off = min(max(o0 + 127 - (k0 & 127) + 1 - kW / 2, 0), lim);
         pred_terms_n<1, false>(ring, r, off, p0, p0, o0, o0, lane, A);
     } else if (np == 2) {
+        kind = 3;
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
         const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
@@ -667,7 +679,12 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const uint8_t *rdl = z.rd + lane;
     const int32_t pb = S.pOff & ~1;  // S.qn: read bytes (pOff >> 1) + lane, + 1
     const int32_t sh = coff - S.pOff;
-    const bool fast = (info & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain && (uint32_t)sh <= 1u;
+    const bool fast = ((S.fmask >> li) & 1u) && (uint32_t)sh <= 1u;
+#ifdef CCSX_DP_STAMPS
+    unsigned long long ts0, ts1, ts2, ts3;
+    int ckind = 0;
+    ROW_STAMP(ts0);
+#endif
     // everything after the predecessor terms; instantiated on both sides of
     // the fast / cold branch so a fast row meets no further branch
     auto tail = [&](int32_t off, uint32_t qp, int32_t Mh0, int32_t Mh1, int32_t Dv0, int32_t Dv1,
@@ -689,6 +706,9 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
             if ((uint32_t)c.L2 + 1 >= m) rk1 = INT32_MIN, Dv1 = kNeg;
         }
         int32_t rk = max(rk0, rk1);
+#ifdef CCSX_DP_STAMPS
+        if (!cold && ckind != 6) ROW_STAMP(ts1);
+#endif
         wave_incl_max2(incl, rk);
         const int32_t Pex = wave_shr1(kNeg, incl);
         int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(max(Pex, X0) + c.cI1, hp1);
@@ -697,11 +717,10 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
             if ((uint32_t)c.L2 + 1 >= m) nH1 = kNegH;
         }
         const int32_t key = __builtin_amdgcn_readlane(rk, 63);
-        // ring row, Pex for the helpers, meta window
+        // ring row, meta window
         int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kHc + c.L2);
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
-        z.lds[kLdsPub + (r % kPubSlots) * 64 + lane] = Pex;
         S.vOff = writelane(S.vOff, off, li);
         S.vKey = writelane(S.vKey, key, li);
         if (cold && (info & kInfoSpill)) {
@@ -720,6 +739,33 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
         S.pOff = off;
         S.pArg = off + 127 - (key & 127);
+#ifdef CCSX_DP_STAMPS
+        if (!cold && ckind != 6) {
+            ROW_STAMP(ts2);
+            ROW_STAMP(ts3);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(ts0), "+s"(ts1), "+s"(ts2), "+s"(ts3)::"memory");
+            z.pf[kPfAHead] += ts1 - t_prev;  // row start -> scan, t_prev: last row's end
+            z.pf[kPfABody] += ts2 - ts1;      // scan and everything after
+            z.pf[kPfATail] += ts0 - t_prev;   // row start -> fast decision
+            z.pf[kPfAFast] += 1;
+            (void)ts3;
+        } else {
+            ROW_STAMP(ts2);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(ts2)::"memory");
+            // constant indices only: a computed index would move z.pf (and
+            // with it much of Z) to scratch
+            const unsigned long long dt = ts2 - t_prev;
+            switch (ckind) {
+            case 0: z.pf[kPfCold0] += dt, z.pf[kPfColdN0] += 1; break;
+            case 1: z.pf[kPfCold1] += dt, z.pf[kPfColdN1] += 1; break;
+            case 2: z.pf[kPfCold2] += dt, z.pf[kPfColdN2] += 1; break;
+            case 3: z.pf[kPfCold3] += dt, z.pf[kPfColdN3] += 1; break;
+            case 4: z.pf[kPfCold4] += dt, z.pf[kPfColdN4] += 1; break;
+            case 5: z.pf[kPfCold5] += dt, z.pf[kPfColdN5] += 1; break;
+            default: z.pf[kPfCold6] += dt, z.pf[kPfColdN6] += 1; break;
+            }
+        }
+#endif
     };
     if (__builtin_expect(fast, 1)) {
         // the only predecessor is row r-1 and the band moved by 0 or 1: its
@@ -734,7 +780,13 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         tail(coff, S.qn >> (4u * (uint32_t)(coff - pb)), Mh0, Mh1, Dv0, Dv1, false);  // coff - pb in [0, 2]
     } else {
         int32_t off, Mh0, Mh1, Dv0, Dv1;
-        dpA_cold(z, S, r, info, coff, lim, off, Mh0, Mh1, Dv0, Dv1);
+        int kind;
+        dpA_cold(z, S, r, info, coff, lim, off, Mh0, Mh1, Dv0, Dv1, kind);
+#ifdef CCSX_DP_STAMPS
+        if (info & kInfoSpill) kind = 5;
+        ckind = kind;
+#endif
+        (void)kind;
         const uint32_t d = (uint32_t)(off - pb);
         const uint32_t qp = d <= 3u ? S.qn >> (4u * d) : (uint32_t)rdl[off >> 1] >> ((uint32_t)(off & 1) * 4u);
         tail(off, qp, Mh0, Mh1, Dv0, Dv1, true);
@@ -749,6 +801,10 @@ __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t
     const int32_t lim = FULL ? (int32_t)m - kW : 0;
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
+    if ((r0 & 63u) == 0) {
+        const uint32_t inf = S.W.cur.info;
+        S.fmask = ballot((inf & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain);
+    }
     dpA_row<FULL>(z, S, r0, lim, m, c);
 #pragma unroll
     for (uint32_t i = 1; i < (uint32_t)kBlkAB; ++i)
@@ -815,7 +871,6 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t np = info >> 8;
     const int32_t off = __builtin_amdgcn_readlane(vOff, li);
-    const int32_t Pex = z.lds[kLdsPub + (r % kPubSlots) * 64 + lane];
     const uint32_t qp = (uint32_t)z.rd[(off >> 1) + lane] >> ((uint32_t)(off & 1) * 4u);
     const int2 Dv = reinterpret_cast<const int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kDc + c.L2)[0];
     PredAcc A;
@@ -845,8 +900,9 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const int32_t M1 = max(A.Mh1, srcu + kE) + (((qp >> 2) & 3u) == base ? kMs : kXs);
     const bool d0 = A.Dv0 > M0, d1 = A.Dv1 > M1;
     const int32_t hp0 = max(M0, A.Dv0), hp1 = max(M1, A.Dv1);
-    // insertions (SPEC.md §3.4) from wave 0's exclusive prefix max
+    // insertions (SPEC.md §3.4): the same prefix-max scan as wave 0's
     const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
+    const int32_t Pex = wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
     const int32_t X1L = wave_shr1(INT32_MAX, X1);
     const int32_t ex1 = max(Pex, X0);
     const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
@@ -1008,7 +1064,7 @@ __device__ __forceinline__ void dp_helper_exit(Z &z)
     __syncthreads();
     // the helper waves hand over their diagnostic counters
     __syncthreads();
-    const volatile unsigned long long *pf1 = reinterpret_cast<const volatile unsigned long long *>(z.lds + kLdsPub);
+    const volatile unsigned long long *pf1 = reinterpret_cast<const volatile unsigned long long *>(z.lds + kLdsDiag);
     for (int h = 0; h < 2; ++h) {
         z.pf[kPfBbusy] += pf1[8 * h + 0];
         z.pf[kPfBwait] += pf1[8 * h + 1];
@@ -1769,7 +1825,7 @@ ccsx_zmw_kernel(KArgs a)
         // waves 1 and 2: the decision bits of the even / odd rows of every DP
         const uint32_t h = uni(threadIdx.x >> 6) - 1u;
         dp_helper(z, h);
-        volatile unsigned long long *pf1 = reinterpret_cast<volatile unsigned long long *>(z.lds + kLdsPub) + 8 * h;
+        volatile unsigned long long *pf1 = reinterpret_cast<volatile unsigned long long *>(z.lds + kLdsDiag) + 8 * h;
         if (lane == 0)
             pf1[0] = z.pf[kPfBbusy], pf1[1] = z.pf[kPfBwait], pf1[2] = z.pf[kPfSpare2], pf1[3] = z.pf[kPfSpare3],
             pf1[4] = z.pf[kPfFlush], pf1[5] = wave_hw_id();

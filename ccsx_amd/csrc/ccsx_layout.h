@@ -21,12 +21,11 @@ constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
 constexpr int kRing = 16;      // DP rows kept in LDS per wave
 constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H and D, each [4 pad | 128 | 4 pad]
 constexpr int kRingA = 24;     // its ring rows: kRing predecessor rows + 2 blocks of the helpers' lag
-constexpr int kPubSlots = 8;   // rows of the insertion prefix max handed from wave 0 to the helpers
 constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-// fixed LDS words per workgroup: DP ring, wave 0 -> waves 1/2 hand-off, band
+// fixed LDS words per workgroup: DP ring, helpers' diagnostic counters, band
 // offsets, job; the read and the shredding cursors follow (ccsx_kernel.hip)
-constexpr int kLdsFixedWords = kRingA * kRowW + kPubSlots * 64 + 64 + 16;
+constexpr int kLdsFixedWords = kRingA * kRowW + 32 + 64 + 16;
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
 enum Status : int32_t {
@@ -169,6 +168,14 @@ enum ProfSlot { kPfTotal = 0, kPfLoad, kPfDp, kPfTrace, kPfMerge, kPfColumns, kP
                 kPfTbProbe, kPfTbStep, kPfTbDI, kPfTbSwitch, kPfTbNsw,
                 // placement: HW_ID | XCC_ID << 32 of waves 0, 1, 2; start / end on
                 // the constant-rate s_memrealtime clock
-                kPfHw0, kPfHw1, kPfHw2, kPfStartRt, kPfEndRt, kProfSlots };
+                kPfHw0, kPfHw1, kPfHw2, kPfStartRt, kPfEndRt,
+                // wave 0 fast rows (diagnostic build): head, body to the scan,
+                // scan to end; number of fast rows
+                kPfAHead, kPfABody, kPfATail, kPfAFast,
+                // wave 0 cold rows by kind (far, chain moved 0..2, one
+                // predecessor, two, other; spill rows; rows on the register
+                // path for predecessors r-1 / r-2): cycles, then counts
+                kPfCold0, kPfCold1, kPfCold2, kPfCold3, kPfCold4, kPfCold5, kPfCold6,
+                kPfColdN0, kPfColdN1, kPfColdN2, kPfColdN3, kPfColdN4, kPfColdN5, kPfColdN6, kProfSlots };
 
 }  // namespace ccsx

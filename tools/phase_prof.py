@@ -31,5 +31,13 @@ out = {"config": vars(a), "kernel_ms": ms, "gcups": cells / ms / 1e6,
                 "b_fast_pred_per_row": round(p["spare2"] / max(p["dp_rows"], 1), 1),
                 "b_cold_pred_per_row": round(p["spare3"] / max(p["dp_rows"], 1), 1),
                 "b_common": round(p["flush"] / max(p["dp_rows"], 1), 1)}}
+nf = max(p["a_fast"], 1)
+out["a_fast_row"] = {"rows_frac": round(p["a_fast"] / max(p["dp_rows"], 1), 4),
+                     "start_to_decision": round(p["a_tail"] / nf, 1),
+                     "start_to_scan": round(p["a_head"] / nf, 1),
+                     "scan_to_end": round(p["a_body"] / nf, 1)}
+out["a_cold_rows"] = {k: {"frac": round(p["n_" + k] / max(p["dp_rows"], 1), 4),
+                          "cycles": round(p["cold_" + k] / max(p["n_" + k], 1), 1)}
+                      for k in ("far", "chain", "np1", "np2", "gen", "spill", "near")}
 out["per_zmw"] = {k: round(v / a.n, 1) for k, v in p.items()}
 print(json.dumps(out))
