@@ -256,7 +256,7 @@ __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
 constexpr int kLdsRing = 0;                              // kRingA DP rows x kRowW (traceback: 2 blocks)
 constexpr int kLdsDiag = kLdsRing + kRingA * kRowW;      // 32: helpers' diagnostic counters at exit
 constexpr int kLdsOffRing = kLdsDiag + 32;               // 64: band offset of DP row q at q & 63
-constexpr int kLdsJob = kLdsOffRing + 64;                // 16: two-wave DP job / results
+constexpr int kLdsJob = kLdsOffRing + 64;                // 16: DP job / results
 constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
 static_assert(kLdsFixed == kLdsFixedWords, "host and device LDS layouts disagree");
@@ -567,6 +567,7 @@ struct AState {
     uint32_t qn;             // read codes at the next row's chain offset (loaded a row ahead)
     uint32_t nspill;         // spill records written
     uint64_t fmask;          // bit q & 63: row q is a chain row without far / spill flags
+    uint32_t ring;           // LDS word offset of this row's ring slot ((r % kRingA) * kRowW)
     RecWin W;
 };
 
@@ -679,7 +680,8 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const uint8_t *rdl = z.rd + lane;
     const int32_t pb = S.pOff & ~1;  // S.qn: read bytes (pOff >> 1) + lane, + 1
     const int32_t sh = coff - S.pOff;
-    const bool fast = ((S.fmask >> li) & 1u) && (uint32_t)sh <= 1u;
+    // (an integer test keeps the branch scalar: a bool of && lowers to a lane mask)
+    const uint32_t fast = (uint32_t)(S.fmask >> li) & ((uint32_t)sh <= 1u ? 1u : 0u);
 #ifdef CCSX_DP_STAMPS
     unsigned long long ts0, ts1, ts2, ts3;
     int ckind = 0;
@@ -718,7 +720,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         }
         const int32_t key = __builtin_amdgcn_readlane(rk, 63);
         // ring row, meta window
-        int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kHc + c.L2);
+        int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + S.ring + kHc + c.L2);
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
         S.vOff = writelane(S.vOff, off, li);
@@ -739,6 +741,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
         S.pOff = off;
         S.pArg = off + 127 - (key & 127);
+        S.ring = S.ring + kRowW == (uint32_t)(kRingA * kRowW) ? 0u : S.ring + kRowW;
 #ifdef CCSX_DP_STAMPS
         if (!cold && ckind != 6) {
             ROW_STAMP(ts2);
@@ -805,10 +808,12 @@ __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t
         const uint32_t inf = S.W.cur.info;
         S.fmask = ballot((inf & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain);
     }
-    dpA_row<FULL>(z, S, r0, lim, m, c);
+    if (r0 + kBlkAB <= z.R) {
 #pragma unroll
-    for (uint32_t i = 1; i < (uint32_t)kBlkAB; ++i)
-        if (r0 + i < z.R) dpA_row<FULL>(z, S, r0 + i, lim, m, c);
+        for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c);
+    } else {
+        for (uint32_t i = 0; r0 + i < z.R; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c);
+    }
     z.lds[kLdsOffRing + lane] = S.vOff;  // band offsets of the last 64 rows for the helpers
     recwin_end(S.W, r0);
 }
@@ -933,14 +938,13 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
 // helper wave h: rows r0 + h + 2i of the block [r0, r0 + kBlkAB); wave 1 also
 // writes the row meta words {band offset | far << 31} of each 16-row group
 template <bool FULL>
-__device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t m, uint32_t h)
+__device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t m, uint32_t h, int32_t vOff)
 {
     const int lane = lane_id();
     const uint32_t R = z.R;
     const int32_t lim = FULL ? (int32_t)m - kW : 0;
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
-    const int32_t vOff = z.lds[kLdsOffRing + lane];
 #pragma unroll
     for (uint32_t i = h; i < (uint32_t)kBlkAB; i += kHelpers)
         if (r0 + i < R) dpB_row<FULL>(z, S, r0 + i, m, lim, vOff, c);
@@ -971,7 +975,7 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
     __syncthreads();  // J: job posted
     AState S;
     S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
-    S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0;
+    S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
     S.qn = (uint32_t)z.rd[lane] | (uint32_t)z.rd[lane + 1] << 8;
     S.nspill = 0;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
@@ -1012,8 +1016,9 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
 #ifdef CCSX_DP_STAMPS
     unsigned long long t_prev = stamp();
 #endif
+    // period b: the decision bits of block b-1
     for (uint32_t b = 0; b <= nblk; ++b) {
-        if (b >= 1 && !z.status) dpB_block<FULL>(z, S, (b - 1) * kBlkAB, m, h);
+        if (b >= 1 && !z.status) dpB_block<FULL>(z, S, (b - 1) * kBlkAB, m, h, z.lds[kLdsOffRing + lane]);
         if (b == nblk) {
             // this wave's candidate: lexicographic (max score, min row, min j)
             const int32_t best = wave_max(S.bE);
@@ -1152,11 +1157,20 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     const uint32_t lane = lane_id();
     uint32_t *ev = P<uint32_t>(z, z.L.ev);
     for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
-    uint32_t r = er, bi = er / kTbRows, buf = 0;
+    uint32_t r = er, bi = er / kTbRows, buf = 0, base = bi * kTbRows;
     int32_t j = (int32_t)ej;
+    // per staged block: lane l < 32 holds the LDS byte address of row
+    // base + l's record for read position 0 (so cell (r, j) sits at
+    // vrow[r - base] + 2 j), farm the block's far rows (tags are slots)
+    uint32_t vrow = 0, farm = 0;
+    auto enter = [&]() {
+        const uint32_t mt = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
+        vrow = buf * (kTbBufWords * 4u) + lane * 256u - 2u * (mt & 0x7FFFFFFFu);
+        farm = (uint32_t)ballot((mt >> 31) != 0u);
+    };
     tb_dma(z, bi, buf);
     __builtin_amdgcn_s_waitcnt(0);
-    uint32_t vmeta = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
+    enter();
     if (bi) tb_dma(z, bi - 1, buf ^ 1u);
     const auto rev = brsrc(ev, m * 4);
     uint32_t vev = 0;                      // events of bases [chunk, chunk + 64), lane = base & 63
@@ -1172,43 +1186,50 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     const uint32_t glim = z.R * 2u + m * 2u + 16u;
     const uint32_t *poff = G_poff(z, z.cur);
     const uint32_t *pred = G_pred(z, z.cur);
-    // the record of cell (r, j); moves to r's block first
+    const uint8_t *lds8 = reinterpret_cast<const uint8_t *>(z.lds);
 #ifdef CCSX_DP_STAMPS
     unsigned long long t_prev = stamp();
 #endif
-    auto cell = [&](uint32_t &mt) -> uint32_t {
-        if (r < bi * kTbRows) {
+    // stage the block holding row r (a switch to the prefetched neighbour
+    // waits only for its DMA)
+    auto to_block = [&]() {
 #ifdef CCSX_DP_STAMPS
-            z.pf[kPfTbNsw] += 1;
-            const unsigned long long ts0 = stamp();
+        z.pf[kPfTbNsw] += 1;
+        const unsigned long long ts0 = stamp();
 #endif
-            const uint32_t nb = r / kTbRows;
-            if (nb + 1 != bi) {
-                __builtin_amdgcn_s_waitcnt(0);
-                tb_dma(z, nb, buf ^ 1u);  // not the prefetched neighbour
-            }
-            bi = nb;
-            buf ^= 1u;
+        const uint32_t nb = r / kTbRows;
+        if (nb + 1 != bi) {
             __builtin_amdgcn_s_waitcnt(0);
-            vmeta = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
-            if (pend >= 0) {
-                __builtin_amdgcn_raw_buffer_store_b32(vpend, rev, lane <= pend_top ? (uint32_t)(pend + (int32_t)lane) * 4u : ~0u,
-                                                      0, 0);
-                pend = -1;
-            }
-            if (bi) tb_dma(z, bi - 1, buf ^ 1u);
-#ifdef CCSX_DP_STAMPS
-            const unsigned long long ts1 = stamp();
-            z.pf[kPfTbSwitch] += ts1 - ts0;
-            t_prev += ts1 - ts0;
-#endif
+            tb_dma(z, nb, buf ^ 1u);  // not the prefetched neighbour
         }
-        mt = (uint32_t)__builtin_amdgcn_readlane((int)vmeta, (int)(r - bi * kTbRows));
-        const int32_t t = j - (int32_t)(mt & 0x7FFFFFFFu);
-        const uint16_t *rb = reinterpret_cast<const uint16_t *>(z.lds + buf * kTbBufWords);
-        return uni((uint32_t)rb[(r - bi * kTbRows) * 128u + (uint32_t)t]);
+        bi = nb;
+        base = bi * kTbRows;
+        buf ^= 1u;
+        __builtin_amdgcn_s_waitcnt(0);
+        enter();
+        if (pend >= 0) {
+            __builtin_amdgcn_raw_buffer_store_b32(vpend, rev, lane <= pend_top ? (uint32_t)(pend + (int32_t)lane) * 4u : ~0u,
+                                                  0, 0);
+            pend = -1;
+        }
+        if (bi) tb_dma(z, bi - 1, buf ^ 1u);
+#ifdef CCSX_DP_STAMPS
+        const unsigned long long ts1 = stamp();
+        z.pf[kPfTbSwitch] += ts1 - ts0;
+        t_prev += ts1 - ts0;
+#endif
+    };
+    // the record of cell (r, j); r must lie in the staged block
+    auto rec_at = [&]() -> uint32_t {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)vrow, (int)(r - base)) + 2u * (uint32_t)j;
+        return uni((uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + a));
+    };
+    auto cell = [&]() -> uint32_t {
+        if (r < base) to_block();
+        return rec_at();
     };
     auto emit = [&](uint32_t e) { vev = (uint32_t)writelane((int)vev, (int)e, j & 63); };
+    // j -= 1, handing a completed 64-base chunk to the store queue
     auto step_j = [&]() {
         if ((j & 63) == 0) {
             if (pend >= 0)
@@ -1220,12 +1241,12 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         }
         --j;
     };
-    auto to_pred = [&](uint32_t mt, uint32_t tag) {
-        if (mt & 0x80000000u) r = uni(pred[uni(poff[r]) + tag]);  // far row: the tag is a slot
+    // to the predecessor given by the cell's tag (a slot on far rows)
+    auto to_pred = [&](uint32_t tag) {
+        if ((farm >> (r - base)) & 1u) r = uni(pred[uni(poff[r]) + tag]);
         else r -= tag;
     };
-    uint32_t mt;
-    uint32_t rec = cell(mt);
+    uint32_t rec = cell();
     for (;;) {
         if (++guard > glim) {
             err = kErrTrace;
@@ -1236,20 +1257,34 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
 #endif
         const uint32_t hc = rec & 3u;
         if (hc == HC_MPRED) {  // state H
-            emit((EV_ALN << 30) | r);
+            // plain steps while the next cell is in the block, the row not
+            // far, no chunk completes and no diagonal run starts
+            for (;;) {
+                emit((EV_ALN << 30) | r);
+                const uint32_t tag = (rec >> 4) & 63u;
+                const uint32_t li = r - base;
+                const uint32_t slow = ((farm >> li) & 1u) | ((j & 63) == 0 ? 1u : 0u) | (tag >= li ? 1u : 0u) |
+                                      ((rec & 0x3F3u) == 0x10u ? 1u : 0u);
+                if (slow) break;
+                --j;
+                r -= tag;
+                rec = rec_at();
+                if ((rec & 3u) != HC_MPRED) break;
+            }
+            if ((rec & 3u) != HC_MPRED) continue;
             bool probed = false;
-            if ((rec & 0x3F3u) == 0x10u && !(mt & 0x80000000u) && (j & 63) != 0 && r > bi * kTbRows) {
+            if ((rec & 0x3F3u) == 0x10u && !((farm >> (r - base)) & 1u) && (j & 63) != 0 && r > base) {
                 // diagonal run: lane i checks that cell (r-1-i, j-1-i) is MPRED to
                 // the row above it, inside this block and this event chunk; the
                 // run's events go into vev by one lane permutation
                 const int32_t i = (int32_t)lane;
-                const int32_t ri = (int32_t)(r - bi * kTbRows) - 1 - i, ji = j - 1 - i;
+                const int32_t ri = (int32_t)(r - base) - 1 - i, ji = j - 1 - i;
                 const bool in = ri >= 0 && (ji & ~63) == chunk;
-                const uint32_t mw = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + (in ? ri : 0)];
-                const int32_t ti = ji - (int32_t)(mw & 0x7FFFFFFFu);
-                const uint16_t *rb = reinterpret_cast<const uint16_t *>(z.lds + buf * kTbBufWords);
-                const uint32_t rc = in && (uint32_t)ti < (uint32_t)kW ? (uint32_t)rb[(uint32_t)ri * 128u + (uint32_t)ti] : 0u;
-                const bool ok = in && (uint32_t)ti < (uint32_t)kW && !(mw & 0x80000000u) && (rc & 0x3F3u) == 0x10u;
+                const uint32_t rb = (uint32_t)__builtin_amdgcn_ds_bpermute((in ? ri : 0) * 4, (int)vrow);
+                const uint32_t ti = (rb + 2u * (uint32_t)ji - (buf * (kTbBufWords * 4u) + (uint32_t)ri * 256u)) >> 1;
+                const bool inb = in && ti < (uint32_t)kW;
+                const uint32_t rc = inb ? (uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + rb + 2u * (uint32_t)ji) : 0u;
+                const bool ok = inb && !((farm >> (uint32_t)(in ? ri : 0)) & 1u) && (rc & 0x3F3u) == 0x10u;
                 const uint64_t bad = ~ballot(ok);
                 const uint32_t k = (uint32_t)__builtin_ctzll(bad);  // cells r-1 .. r-k continue the run (k < 64)
                 // base b = j - 1 - i gets ALN | (r - 1 - i): lane b & 63 reads lane (j - 1 - b) & 63
@@ -1267,8 +1302,8 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 probed = true;
             }
             step_j();
-            to_pred(mt, (rec >> 4) & 63u);
-            rec = cell(mt);
+            to_pred((rec >> 4) & 63u);
+            rec = cell();
             if (probed) DP_STAMP(kPfTbProbe);
             else DP_STAMP(kPfTbStep);
             (void)probed;
@@ -1284,8 +1319,8 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             // state D: follow D tags while the cell's D extends its predecessor's D
             for (;;) {
                 const uint32_t ext = rec & 4u;
-                to_pred(mt, (rec >> 10) & 63u);
-                rec = cell(mt);
+                to_pred((rec >> 10) & 63u);
+                rec = cell();
                 if (!ext || ++guard > glim) break;
             }
             DP_STAMP(kPfTbDI);
@@ -1296,7 +1331,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             emit((EV_INS << 30) | r);
             const uint32_t ext = rec & 8u;
             step_j();
-            rec = cell(mt);
+            rec = rec_at();
             if (!ext || ++guard > glim) break;
         }
         DP_STAMP(kPfTbDI);

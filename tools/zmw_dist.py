@@ -29,7 +29,9 @@ out = {"kernel_ms": ms, "plain_ms": plain, "n": n, "mean": sum(tot) / n, "min": 
        "max": tot[-1], "max_over_mean": tot[-1] / (sum(tot) / n),
        "slowest": [{"zmw": i, "segs": len(zs[i].lens), "bases": int(sum(zs[i].lens)),
                     **{k: pz[i][k] for k in ("total", "dp", "traceback", "merge", "dp_rows")}} for i in slow],
-       "mean_bases": sum(int(sum(z.lens)) for z in zs) / n}
+       "mean_bases": sum(int(sum(z.lens)) for z in zs) / n,
+       "mean_phase": {k: round(sum(p[k] for p in pz) / n / 1e6, 2) for k in
+                      ("total", "load_read", "dp", "traceback", "merge", "columns", "shred", "dp_rows")}}
 
 
 def simd(v):  # HW_ID: simd 5:4, cu 11:8, sh 12, se 15:13; XCC_ID in bits 32+
