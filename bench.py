@@ -141,11 +141,6 @@ def main():
     eng.stage(zs)
     for _ in range(args.warmup):
         eng.launch(cfg["mode"])
-    res = eng.fetch()
-    cells_per_step = sum(r[2] for r in res)
-    bad = [i for i, r in enumerate(res) if r[1] != 0]
-    if bad:
-        raise SystemExit(f"device status != 0 for {len(bad)} ZMWs")
 
     def barrier():
         if dist is not None:
@@ -158,6 +153,13 @@ def main():
         kernel_ms.append(eng.launch(cfg["mode"]))  # synchronises on the stream's end event
     t1 = time.perf_counter()
     barrier()
+    # results of the last step: status check and the cell count (read back
+    # after the timed region so the warmup and timed launches run back to back)
+    res = eng.fetch()
+    cells_per_step = sum(r[2] for r in res)
+    bad = [i for i, r in enumerate(res) if r[1] != 0]
+    if bad:
+        raise SystemExit(f"device status != 0 for {len(bad)} ZMWs")
     elapsed = t1 - t0
     elapsed, cells_total_step = aggregate(dist, elapsed, cells_per_step)
 

@@ -38,8 +38,10 @@ lines = [f"# rocprofv3 summary `{tag}` — {bench['config']['workload']}", "",
          "| kernel | calls | avg ns | min ns | max ns |", "|---|---|---|---|---|"]
 for s in stats:
     lines.append(f"| `{s['Name'][:60]}` | {s['Calls']} | {float(s['AverageNs']):.0f} | {s['MinNs']} | {s['MaxNs']} |")
-lines += ["", f"bench.py (same run): avg launch {bench['roofline']['avg_launch_ms']} ms (HIP events); "
-          f"rocprof avg {avg_ns / 1e6:.3f} ms.", "", "## PMC (per launch of ccsx_zmw_kernel)", "",
+lines += ["", f"bench.py (same run, {bench['warmup']} warmup + {bench['steps']} timed launches): avg timed launch "
+          f"{bench['roofline']['avg_launch_ms']} ms (HIP events), steps {bench.get('step_ms')}; rocprof avg over all "
+          f"launches {avg_ns / 1e6:.3f} ms (includes the cold first launch).", "",
+          "## PMC (per launch of ccsx_zmw_kernel, one-launch runs)", "",
           "| counter | value |", "|---|---|"]
 for n in sorted(c):
     lines.append(f"| {n} | {c[n]:.4g} |")
