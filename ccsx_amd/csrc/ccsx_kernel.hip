@@ -1042,7 +1042,9 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
     }
 }
 
+template <bool LM>
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid);
+__device__ __forceinline__ bool merge_in_lds(uint32_t R);
 
 // helper wave h (1 + h = wave index): serve DP and merge jobs until wave 0
 // posts kJobExit
@@ -1057,7 +1059,10 @@ __device__ __forceinline__ void dp_helper(Z &z, uint32_t h)
         z.cur = uni((int)job->cur);
         z.status = kOk;
         const uint32_t m = uni(job->m);
-        if (kind == kJobMerge) merge(z, uni(job->k), m, threadIdx.x);
+        if (kind == kJobMerge) {
+            if (merge_in_lds(z.R)) merge<true>(z, uni(job->k), m, threadIdx.x);
+            else merge<false>(z, uni(job->k), m, threadIdx.x);
+        }
         else if (m >= (uint32_t)kW) dp_wave_b<true>(z, m, h);
         else dp_wave_b<false>(z, m, h);
     }
@@ -1396,6 +1401,14 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
 // workgroup barriers (which also make the HBM writes visible); M1's ordered
 // compaction and the two prefix scans run on wave 0 between barriers.  Every
 // branch that skips a barrier is uniform over the workgroup.
+// LM: the graph is small enough (every shredding window) for the current
+// rows' node bytes and the new-row counts / shifts to live in the DP ring's
+// LDS (idle during merge): the column walks, the count atomics, the prefix
+// scan and every shift lookup are then LDS accesses instead of dependent HBM
+// round trips.  Larger graphs (-P) take the same steps through HBM.
+__device__ __forceinline__ bool merge_in_lds(uint32_t R) { return (R + 1) * 5u + 64u <= (uint32_t)(kRingA * kRowW * 4); }
+
+template <bool LM>
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid)
 {
     constexpr uint32_t T = kBlockThreads;
@@ -1404,7 +1417,16 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     volatile DpJob *job = dp_job(z);
     const uint32_t R = z.R, nw = z.d.nw;
     const int a = z.cur, b = a ^ 1;
-    const uint8_t *nb = G_nb(z, a);
+    const uint8_t *nbg = G_nb(z, a);
+    uint32_t *lcnt = reinterpret_cast<uint32_t *>(z.lds + kLdsRing);  // LM: counts / shifts, R + 1 words
+    uint8_t *lnb = reinterpret_cast<uint8_t *>(lcnt + R + 1);          // LM: node bytes, R (+ 3) bytes
+    if (LM) {
+        for (uint32_t x = tid; x <= R; x += T) lcnt[x] = 0;
+        for (uint32_t x = 4 * tid; x < R; x += 4 * T)
+            *reinterpret_cast<uint32_t *>(lnb + x) = *reinterpret_cast<const uint32_t *>(nbg + x);
+        __syncthreads();
+    }
+    const uint8_t *nb = LM ? lnb : nbg;
     const uint64_t *mem = G_mem(z, a);
     const uint32_t *poff = G_poff(z, a);
     const uint32_t *pred = G_pred(z, a);
@@ -1417,7 +1439,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     uint32_t *ipt = P<uint32_t>(z, z.L.ipt);
     uint8_t *iinf = P<uint8_t>(z, z.L.iinf);
     uint32_t *ifix = P<uint32_t>(z, z.L.ifix);
-    uint32_t *cnt = P<uint32_t>(z, z.L.cnt);
+    uint32_t *cnt = LM ? lcnt : P<uint32_t>(z, z.L.cnt);
     uint8_t *fixf = P<uint8_t>(z, z.L.fixf);
     uint32_t *addp = P<uint32_t>(z, z.L.addp);
     uint32_t *cntn = P<uint32_t>(z, z.L.cntn);
@@ -1487,7 +1509,10 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     }
     DP_STAMP(kPfRowA);
     // M2: shift[x] = #new items with point <= x
-    for (uint32_t x = tid; x <= R; x += T) cnt[x] = 0, fixf[x] = 0;
+    for (uint32_t x = tid; x <= R; x += T) {
+        if (!LM) cnt[x] = 0;
+        fixf[x] = 0;
+    }
     __syncthreads();
     for (uint32_t i = tid; i < K; i += T) {
         atomicAdd(&cnt[ipt[i]], 1u);
@@ -1721,7 +1746,8 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             volatile DpJob *job = dp_job(z);
             if (lane_id() == 0) job->kind = kJobMerge, job->m = m, job->R = z.R, job->cur = (uint32_t)z.cur, job->k = k;
             __syncthreads();  // J: job posted
-            merge(z, k, m, threadIdx.x);
+            if (merge_in_lds(z.R)) merge<true>(z, k, m, threadIdx.x);
+            else merge<false>(z, k, m, threadIdx.x);
         }
         if (z.status) return 0;
         z.pf[kPfMerge] += stamp() - t1;
