@@ -1529,28 +1529,75 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     // M3: at most one new in-edge per target of this read (dedup vs existing)
     for (uint32_t x = tid; x < R2; x += T) addp[x] = kNone;
     __syncthreads();
-    for (uint32_t j = 1 + tid; j < m; j += T) {
-        const uint32_t s = tgt[j - 1], d = tgt[j];
-        bool dup = false;
-        if (!(d & kNewBit) && !(s & kNewBit)) {
-            const uint32_t e1 = poff[d + 1];
-            for (uint32_t e = poff[d]; e < e1; ++e)
-                if (pred[e] == s) {
-                    dup = true;
-                    break;
-                }
+    // (MB read bases per thread per pass: their dependent loads are issued
+    // together so the HBM round trips overlap)
+    constexpr uint32_t MB = 4;
+    for (uint32_t j0 = 1 + tid; j0 < m; j0 += MB * T) {
+        uint32_t sv[MB], dv[MB], e0[MB], e1[MB], p0[MB], p1[MB];
+#pragma unroll
+        for (uint32_t b = 0; b < MB; ++b) {
+            const uint32_t j = j0 + b * T;
+            sv[b] = j < m ? tgt[j - 1] : kNewBit;
+            dv[b] = j < m ? tgt[j] : kNewBit;
         }
-        if (!dup) addp[newidx(d)] = newidx(s);
+#pragma unroll
+        for (uint32_t b = 0; b < MB; ++b) {
+            const bool old = !(dv[b] & kNewBit) && !(sv[b] & kNewBit);
+            e0[b] = old ? poff[dv[b]] : 0u;
+            e1[b] = old ? poff[dv[b] + 1] : 0u;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < MB; ++b) {
+            p0[b] = e0[b] < e1[b] ? pred[e0[b]] : kNone;
+            p1[b] = e0[b] + 1 < e1[b] ? pred[e0[b] + 1] : kNone;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < MB; ++b) {
+            const uint32_t j = j0 + b * T;
+            if (j >= m) continue;
+            const uint32_t s = sv[b], d = dv[b];
+            bool dup = p0[b] == s || p1[b] == s;
+            for (uint32_t e = e0[b] + 2; !dup && e < e1[b]; ++e) dup = pred[e] == s;
+            if (!dup) addp[newidx(d)] = newidx(s);
+        }
     }
     __syncthreads();
     DP_STAMP(kPfRowC);
     // M4: rows of the new graph
-    for (uint32_t x = tid; x < R; x += T) {
-        const uint32_t n = x + shift[x];
-        nb2[n] = fixf[x] ? (uint8_t)(nb[x] & 3u) : nb[x];
-        spf[n] = 0;
-        for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = mem[(size_t)x * nw + w];
-        cntn[n] = poff[x + 1] - poff[x] + (addp[n] != kNone ? 1u : 0u);
+    if (nw == 1) {
+        for (uint32_t x0 = tid; x0 < R; x0 += MB * T) {
+            uint32_t n[MB], fx[MB], e0[MB], e1[MB], nbx[MB], ad[MB];
+            uint64_t mw[MB];
+#pragma unroll
+            for (uint32_t b = 0; b < MB; ++b) {
+                const uint32_t x = x0 + b * T;
+                const bool v = x < R;
+                n[b] = v ? x + shift[x] : 0u;
+                fx[b] = v ? fixf[x] : 0u;
+                nbx[b] = v ? nb[x] : 0u;
+                e0[b] = v ? poff[x] : 0u;
+                e1[b] = v ? poff[x + 1] : 0u;
+                mw[b] = v ? mem[x] : 0ull;
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < MB; ++b) ad[b] = x0 + b * T < R ? addp[n[b]] : kNone;
+#pragma unroll
+            for (uint32_t b = 0; b < MB; ++b) {
+                if (x0 + b * T >= R) continue;
+                nb2[n[b]] = fx[b] ? (uint8_t)(nbx[b] & 3u) : (uint8_t)nbx[b];
+                spf[n[b]] = 0;
+                mem2[n[b]] = mw[b];
+                cntn[n[b]] = e1[b] - e0[b] + (ad[b] != kNone ? 1u : 0u);
+            }
+        }
+    } else {
+        for (uint32_t x = tid; x < R; x += T) {
+            const uint32_t n = x + shift[x];
+            nb2[n] = fixf[x] ? (uint8_t)(nb[x] & 3u) : nb[x];
+            spf[n] = 0;
+            for (uint32_t w = 0; w < nw; ++w) mem2[(size_t)n * nw + w] = mem[(size_t)x * nw + w];
+            cntn[n] = poff[x + 1] - poff[x] + (addp[n] != kNone ? 1u : 0u);
+        }
     }
     for (uint32_t i = tid; i < K; i += T) {
         const uint32_t n = ipt[i] + i;
@@ -1582,19 +1629,40 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     // {base | chain << 3 | np << 8, p0, p1, p2} + p3 (dp_fast's prefetch)
     uint4 *rrec = P<uint4>(z, z.L.rrec);
     uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
-    for (uint32_t x = tid; x < R; x += T) {
-        const uint32_t n = x + shift[x];
-        const uint32_t e0 = poff[x], e1 = poff[x + 1];
-        const uint32_t ad = addp[n];
-        uint32_t o = poff2[n];
+    // (PB rows per thread per pass, loads first)
+    constexpr uint32_t PB = 2;
+    for (uint32_t x0 = tid; x0 < R; x0 += PB * T) {
+      uint32_t bn[PB], be0[PB], be1[PB], bad[PB], bo[PB], bq[PB][4];
+#pragma unroll
+      for (uint32_t b = 0; b < PB; ++b) {
+          const uint32_t x = x0 + b * T;
+          const bool v = x < R;
+          bn[b] = v ? x + shift[x] : 0u;
+          be0[b] = v ? poff[x] : 0u;
+          be1[b] = v ? poff[x + 1] : 0u;
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < PB; ++b) {
+          const bool v = x0 + b * T < R;
+          bad[b] = v ? addp[bn[b]] : kNone;
+          bo[b] = v ? poff2[bn[b]] : 0u;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) bq[b][u] = be0[b] + u < be1[b] ? pred[be0[b] + u] : 0u;
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < PB; ++b) {
+        const uint32_t x = x0 + b * T;
+        if (x >= R) continue;
+        const uint32_t n = bn[b];
+        const uint32_t e0 = be0[b], e1 = be1[b];
+        const uint32_t ad = bad[b];
+        uint32_t o = bo[b];
         const uint32_t ne = e1 - e0;
         const uint32_t np = ne + (ad != kNone ? 1u : 0u);
-        // the first four old predecessors, loaded together, then their shifts
+        // the first four old predecessors (loaded above), then their shifts
         uint32_t q[4], ps[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) q[u] = (uint32_t)u < ne ? pred[e0 + u] : 0u;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) q[u] = (uint32_t)u < ne ? q[u] + shift[q[u]] : 0u;
+        for (int u = 0; u < 4; ++u) q[u] = (uint32_t)u < ne ? bq[b][u] + shift[bq[b][u]] : 0u;
         uint32_t far = np > 4u ? kInfoFar : 0u;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1618,6 +1686,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
         const uint32_t chain = (np == 1 && ps[0] + 1 == n) ? kInfoChain : 0u;
         rrec[n] = make_uint4((nb[x] & 3u) | chain | far | (np << 8), ps[0], ps[1], ps[2]);
         rp3[n] = ps[3];
+      }
     }
     for (uint32_t i = tid; i < K; i += T) {
         const uint32_t n = ipt[i] + i;
