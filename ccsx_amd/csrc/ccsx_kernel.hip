@@ -1181,10 +1181,22 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     // base + l's record for read position 0 (so cell (r, j) sits at
     // vrow[r - base] + 2 j), farm the block's far rows (tags are slots)
     uint32_t vrow = 0, farm = 0;
+#ifndef CCSX_TB_NOWIN
+    // record window of the plain MPRED steps: lane l holds the records of
+    // block row l & 31 at columns jw - 1 - 2 (l >> 5) (low half) and the
+    // column below it (high half), i.e. four columns of every staged row;
+    // valid while j lies in [jw - 4, jw) (entering a block invalidates it)
+    uint32_t vrow32 = 0, win = 0;
+    int32_t jw = INT32_MIN / 2;
+#endif
     auto enter = [&]() {
         const uint32_t mt = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
         vrow = buf * (kTbBufWords * 4u) + lane * 256u - 2u * (mt & 0x7FFFFFFFu);
         farm = (uint32_t)ballot((mt >> 31) != 0u);
+#ifndef CCSX_TB_NOWIN
+        vrow32 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & 31u) * 4u), (int)vrow) - ((lane >> 5) * 4u);
+        jw = INT32_MIN / 2;
+#endif
     };
     tb_dma(z, bi, buf);
     __builtin_amdgcn_s_waitcnt(0);
@@ -1281,12 +1293,35 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 emit((EV_ALN << 30) | r);
                 const uint32_t tag = (rec >> 4) & 63u;
                 const uint32_t li = r - base;
+#ifdef CCSX_TB_NOWIN
                 const uint32_t slow = ((farm >> li) & 1u) | ((j & 63) == 0 ? 1u : 0u) | (tag >= li ? 1u : 0u) |
                                       ((rec & 0x3F3u) == 0x10u ? 1u : 0u);
+#else
+                // sign-bit arithmetic keeps the test on the scalar unit (a
+                // compare of a bool lowers to VALU selects): far row, a chunk
+                // completes ((j & 63) == 0), or the predecessor leaves the block
+                const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag - 1u) >> 31)) & 1u;
+#endif
                 if (slow) break;
                 --j;
                 r -= tag;
+#ifdef CCSX_TB_NOWIN
                 rec = rec_at();
+#else
+                // r stays inside the block (tag < li): the next record comes
+                // from the window by one readlane; an LDS round trip only
+                // every fourth column
+                uint32_t k = (uint32_t)(jw - 1 - j);
+                if (k >= 4u) {
+                    const uint32_t a = vrow32 + 2u * (uint32_t)j;
+                    const uint32_t lo = *reinterpret_cast<const uint16_t *>(lds8 + a);
+                    const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds8 + a - 2u);
+                    win = lo | hi << 16;
+                    jw = j + 1, k = 0;
+                }
+                rec = ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((k & 2u) << 4))) >>
+                       ((k & 1u) * 16u)) & 0xFFFFu;
+#endif
                 if ((rec & 3u) != HC_MPRED) break;
             }
             if ((rec & 3u) != HC_MPRED) continue;
