@@ -38,9 +38,20 @@ lines = [f"# rocprofv3 summary `{tag}` — {bench['config']['workload']}", "",
          "| kernel | calls | avg ns | min ns | max ns |", "|---|---|---|---|---|"]
 for s in stats:
     lines.append(f"| `{s['Name'][:60]}` | {s['Calls']} | {float(s['AverageNs']):.0f} | {s['MinNs']} | {s['MaxNs']} |")
+# per-dispatch durations of the kernel: the last `steps` dispatches are the
+# launches bench.py timed (its warmup launches come first)
+durs = []
+for f in glob.glob(os.path.join(src, "kt", "*kernel_trace.csv")):
+    for row in csv.DictReader(open(f)):
+        if KERNEL in row["Kernel_Name"]:
+            durs.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+durs = [d for _, d in sorted(durs)]
+timed = durs[-int(bench["steps"]):] if durs else []
+timed_ms = sum(timed) / len(timed) / 1e6 if timed else float("nan")
 lines += ["", f"bench.py (same run, {bench['warmup']} warmup + {bench['steps']} timed launches): avg timed launch "
           f"{bench['roofline']['avg_launch_ms']} ms (HIP events), steps {bench.get('step_ms')}; rocprof avg over all "
-          f"launches {avg_ns / 1e6:.3f} ms (includes the cold first launch).", "",
+          f"launches {avg_ns / 1e6:.3f} ms (includes the cold first launch); rocprof avg over the "
+          f"{len(timed)} timed launches {timed_ms:.3f} ms (kernel trace).", "",
           "## PMC (per launch of ccsx_zmw_kernel, one-launch runs)", "",
           "| counter | value |", "|---|---|"]
 for n in sorted(c):
