@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <string>
 #include <thread>
 #include <unordered_set>
@@ -186,11 +187,12 @@ int main(int argc, char **argv)
         if (ccsx_gpu_open(g, &ctx[g]) != 0) return 1;
     if (nthreads < 1) nthreads = 1;
 
-    // main.c:652-697 (step 0), 698-706 (step 1), 707-717 (step 2)
+    // main.c:652-697 (step 0), 698-706 (step 1), 707-717 (step 2).  As the
+    // reference's kt_pipeline overlaps step 0 of the next chunk with step 1,
+    // chunk k + 1 is read and prepared on the CPU while the GPUs run chunk k;
+    // chunks are written in input order.
     size_t chunk_size = 1024;
-    int rc = 0;
-    for (;;) {
-        std::vector<Zmw> zs;
+    auto read_chunk = [&](std::vector<Zmw> &zs) -> bool {
         const char *movie, *hole, *seqs;
         const uint32_t *lens;
         int l;
@@ -212,19 +214,32 @@ int main(int argc, char **argv)
         }
         // kt_pipeline stops on an empty chunk (main.c:694-697); a chunk cut
         // short by -1 (end of input or an invalid name) is processed and the
-        // next iteration reads on, as the reference's next step 0 does
-        if (zs.empty()) break;
+        // next call reads on, as the reference's next step 0 does
+        if (zs.empty()) return false;
         prepare_chunk(zs, nthreads, verbose);
+        return true;
+    };
+    int rc = 0;
+    std::vector<Zmw> cur;
+    bool have = read_chunk(cur);
+    while (have) {
+        std::vector<Zmw> nxt;
+        std::future<bool> ahead = std::async(std::launch::async, [&]() { return read_chunk(nxt); });
         if (verbose > 1)
-            for (auto &z : zs) fprintf(stderr, "poa begin %s\n", z.hole.c_str());
-        if (!run_chunk(zs, ctx, split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE)) {
+            for (auto &z : cur) fprintf(stderr, "poa begin %s\n", z.hole.c_str());
+        const bool ok = run_chunk(cur, ctx, split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE);
+        if (ok) {
+            for (auto &z : cur) {
+                if (verbose > 1) fprintf(stderr, "poa end %s\n", z.hole.c_str());
+                if (!z.ccs.empty()) fprintf(fp_out, ">%s/%s/ccs\n%s\n", z.movie.c_str(), z.hole.c_str(), z.ccs.c_str());
+            }
+        }
+        have = ahead.get();
+        if (!ok) {
             rc = 1;
             break;
         }
-        for (auto &z : zs) {
-            if (verbose > 1) fprintf(stderr, "poa end %s\n", z.hole.c_str());
-            if (!z.ccs.empty()) fprintf(fp_out, ">%s/%s/ccs\n%s\n", z.movie.c_str(), z.hole.c_str(), z.ccs.c_str());
-        }
+        cur.swap(nxt);
     }
     for (auto *x : ctx) ccsx_gpu_close(x);
     ccsx_reader_close(rd);

@@ -43,3 +43,17 @@ def test_cli_matches_oracle(tmp_path, mode_flag, mode):
     got = open(out, "rb").read()
     assert got == _expected(fa, mode, exclude={"3", "5"})
     assert got.count(b">") == 10
+
+
+def test_cli_multi_chunk_order(tmp_path):
+    """1,100 ZMWs: more than the first 1,024-ZMW chunk (main.c:686-690), so the
+    second chunk is read and prepared while the GPU runs the first; the output
+    stays in input order and equal to the oracle's."""
+    fa = str(tmp_path / "in.fa")
+    write(fa, 1100, 1000, 6)
+    out = str(tmp_path / "out.fa")
+    r = subprocess.run([BIN, "-A", "-j", "4", fa, out], capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    got = open(out, "rb").read()
+    assert got.count(b">") == 1100
+    assert got == _expected(fa, 0)
