@@ -77,13 +77,16 @@ def build_product(verbose: bool = False) -> str:
         os.path.join(CSRC, "host", "seqio.cpp"),
     ]
     common = ["-O3", "-std=c++17", "-fPIC", "-I" + INC, "-I" + CSRC, "-I" + os.path.join(CSRC, "host")]
+    # the kernel's per-ZMW chains are latency-bound: the ILP-maximising machine
+    # scheduler measured -0.8 % per launch on config B (tools/abn.sh)
+    kflags = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
     objs = []
     for s in srcs:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
         if _stale(o, [s] + hdrs):
             if s.endswith(".hip"):
-                cmd = [hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + ["-c", s, "-o", o]
+                cmd = [hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + ["-c", s, "-o", o]
             else:
                 cmd = [hipcc, "-x", "c++"] + common + ["-D__HIP_PLATFORM_AMD__", "-I" + _rocm_inc(), "-c", s, "-o", o]
             if verbose:
@@ -101,7 +104,7 @@ def build_product(verbose: bool = False) -> str:
         # the stamps' counters need registers: 2 waves per SIMD (occupancy is
         # not what this build measures; per-ZMW cycle counts are)
         _run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2"] + common
-             + ["-c", srcs[0], "-o", dobj])
+             + kflags + ["-c", srcs[0], "-o", dobj])
     if _stale(diag, objs[1:] + [dobj]):
         _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", diag, dobj] + objs[1:] + ["-lz", "-lpthread"])
     # the C host program
