@@ -7,6 +7,7 @@
 // of ccsx's pipeline (main.c:698-706).
 #include "ccsx_gpu.h"
 
+#include <chrono>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,8 +31,17 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t c = std::max<size_t>(n, 256);
+        // grow with 25 % headroom (falling back to the exact size): slices of
+        // one chunk differ by a few percent, and re-allocating a workspace a
+        // full launch has touched measured 1-5 s per 75-150 GB (DESIGN.md
+        // section 7)
+        size_t c = std::max<size_t>(n + n / 4, 256);
         hipError_t e = hipMalloc(&p, c);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            c = std::max<size_t>(n, 256);
+            e = hipMalloc(&p, c);
+        }
         if (e == hipSuccess) cap = c;
         return e;
     }
@@ -63,6 +73,8 @@ struct ccsx_ctx {
     std::vector<ccsx::ZmwDesc> desc;
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
+    uint32_t mem_share = 1;            // contexts sharing the device concurrently
+    bool prealloc = false;             // reserve the slice budget up front
     std::vector<uint8_t> run_arena;    // ccsx_gpu_run's gathered CCS strings
     DevBuf d_prof;
     std::vector<unsigned long long> h_prof;
@@ -223,6 +235,9 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
         c->err = m;
         return -1;
     }
+    const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
+    using tms = std::chrono::duration<double, std::milli>;
+    const auto ta = std::chrono::steady_clock::now();
     HIPCHK(c, c->d_seq.reserve(seq_b));
     HIPCHK(c, c->d_soff.reserve(size_t(nseg) * 4));
     HIPCHK(c, c->d_slen.reserve(size_t(nseg) * 4));
@@ -235,6 +250,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, c->d_ncols.reserve(nz * 4));
     HIPCHK(c, c->d_status.reserve(nz * 4));
     HIPCHK(c, c->d_cells.reserve(nz * 8));
+    const auto tb = std::chrono::steady_clock::now();
     // host staging of the sequence arena and segment tables
     std::vector<uint8_t> hseq(seq_b);
     std::vector<uint32_t> hoff(nseg), hlen(nseg);
@@ -263,6 +279,9 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     });
     HIPCHK(c, hipMemcpyAsync(c->d_order.p, order.data(), nz * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (timing)
+        fprintf(stderr, "[ccsx_gpu_stage] %zu ZMWs: reserve %.0f ms (ws cap %.1f GB), pack+copy %.1f MB %.0f ms\n", nz,
+                tms(tb - ta).count(), c->d_ws.cap / 1e9, seq_b / 1e6, tms(std::chrono::steady_clock::now() - tb).count());
     return 0;
 }
 
@@ -373,7 +392,19 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     size_t freeb = 0, totb = 0;
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
     const uint64_t held = c->d_ws.cap + c->d_seq.cap + c->d_out.cap + c->d_msa.cap;
-    const uint64_t budget = freeb + held > (3ull << 30) ? freeb + held - (3ull << 30) : (1ull << 30);
+    uint64_t budget = freeb + held > (3ull << 30) ? freeb + held - (3ull << 30) : (1ull << 30);
+    {
+        // at most half the device per context (and a fixed share of it when
+        // contexts run concurrently, so they cannot both size themselves to
+        // the same free memory): a slice of half the device already holds
+        // ~7k mixed-size ZMWs, several times the resident workgroups, while
+        // allocating up to the last free GB measured 6.3 s of staging for a
+        // 305 GB slice vs 0.18 s for 84 GB
+        const uint64_t part = totb / (2ull * c->mem_share);
+        budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
+    }
+    if (c->prealloc && c->d_ws.cap < budget) HIPCHK(c, c->d_ws.reserve(budget));
+    const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     c->run_arena.clear();
     std::vector<uint64_t> aoff(nz, 0);
     std::string first_err;
@@ -390,13 +421,22 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             }
             std::vector<ccsx_zmw_in> sub(e - b);
             for (size_t i = b; i < e; ++i) sub[i - b] = z[idx[i]];
+            const auto t0 = std::chrono::steady_clock::now();
             int r = ccsx_gpu_stage_ex(c, sub.data(), sub.size(), 0, full ? 1 : 0);
             if (r) return r;
-            r = ccsx_gpu_launch_ex(c, mode, nullptr);
+            const auto t1 = std::chrono::steady_clock::now();
+            float kms = 0.f;
+            r = ccsx_gpu_launch_ex(c, mode, timing ? &kms : nullptr);
             if (r) return r;
             std::vector<ccsx_zmw_out> o(sub.size());
             r = ccsx_gpu_fetch(c, o.data());
             if (r && r != -2) return r;
+            if (timing) {
+                using ms = std::chrono::duration<double, std::milli>;
+                fprintf(stderr, "[ccsx_gpu_run] dev %d slice %zu ZMWs (%s caps, %.1f GB budget %.1f GB): stage %.0f ms, "
+                        "kernel %.0f ms, launch+fetch %.0f ms\n", c->device, sub.size(), full ? "full" : "tight",
+                        need / 1e9, budget / 1e9, ms(t1 - t0).count(), kms, ms(std::chrono::steady_clock::now() - t1).count());
+            }
             for (size_t i = 0; i < sub.size(); ++i) {
                 const uint32_t g = idx[b + i];
                 out[g].cells = o[i].cells;
@@ -438,6 +478,20 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *c, uint32_t rows)
 {
     if (!c) return -1;
     c->tight_rows = rows;
+    return 0;
+}
+
+int ccsx_gpu_set_mem_share(ccsx_ctx *c, uint32_t share)
+{
+    if (!c || share == 0) return -1;
+    c->mem_share = share;
+    return 0;
+}
+
+int ccsx_gpu_set_prealloc(ccsx_ctx *c, int on)
+{
+    if (!c) return -1;
+    c->prealloc = on != 0;
     return 0;
 }
 

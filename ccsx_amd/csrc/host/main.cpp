@@ -9,6 +9,7 @@
 #include <getopt.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -182,9 +183,21 @@ int main(int argc, char **argv)
         return 1;
     }
     if (const char *e = getenv("CCSX_NGPU")) ndev = std::max(1, std::min(ndev, atoi(e)));
-    std::vector<ccsx_ctx *> ctx(ndev, nullptr);
-    for (int g = 0; g < ndev; ++g)
-        if (ccsx_gpu_open(g, &ctx[g]) != 0) return 1;
+    // CCSX_SLOTS=2: two chunk slots per GPU, each with its own context and
+    // stream, chunk k + 1 launched on the other slot while chunk k drains (so
+    // the CUs its finished workgroups free could take chunk k + 1's work).
+    // Measured slower on MI355X (the concurrent chunk's
+    // staging stalls the running one), so one chunk in flight is the default;
+    // with one slot, chunk k + 1 is launched before chunk k is written out.
+    int nslot = 1;
+    if (const char *e = getenv("CCSX_SLOTS")) nslot = std::max(1, std::min(2, atoi(e)));
+    std::vector<std::vector<ccsx_ctx *>> ctx(nslot, std::vector<ccsx_ctx *>(ndev, nullptr));
+    for (int s = 0; s < nslot; ++s)
+        for (int g = 0; g < ndev; ++g) {
+            if (ccsx_gpu_open(g, &ctx[s][g]) != 0) return 1;
+            ccsx_gpu_set_mem_share(ctx[s][g], (uint32_t)nslot);
+            ccsx_gpu_set_prealloc(ctx[s][g], 1);
+        }
     if (nthreads < 1) nthreads = 1;
 
     // main.c:652-697 (step 0), 698-706 (step 1), 707-717 (step 2).  As the
@@ -192,7 +205,14 @@ int main(int argc, char **argv)
     // chunk k + 1 is read and prepared on the CPU while the GPUs run chunk k;
     // chunks are written in input order.
     size_t chunk_size = 1024;
+    // CCSX_TIMING=1: per-chunk wall-clock phases on stderr (ms since start)
+    const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
+    const auto tstart = std::chrono::steady_clock::now();
+    auto now_ms = [tstart]() {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tstart).count();
+    };
     auto read_chunk = [&](std::vector<Zmw> &zs) -> bool {
+        const double t0 = now_ms();
         const char *movie, *hole, *seqs;
         const uint32_t *lens;
         int l;
@@ -216,32 +236,61 @@ int main(int argc, char **argv)
         // short by -1 (end of input or an invalid name) is processed and the
         // next call reads on, as the reference's next step 0 does
         if (zs.empty()) return false;
+        const double t1 = now_ms();
         prepare_chunk(zs, nthreads, verbose);
+        if (timing)
+            fprintf(stderr, "[ccsx] chunk %zu ZMWs: read %.0f-%.0f ms, prepare until %.0f ms\n", zs.size(), t0, t1,
+                    now_ms());
         return true;
     };
     int rc = 0;
-    std::vector<Zmw> cur;
-    bool have = read_chunk(cur);
-    while (have) {
-        std::vector<Zmw> nxt;
-        std::future<bool> ahead = std::async(std::launch::async, [&]() { return read_chunk(nxt); });
+    const int mode = split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE;
+    std::vector<Zmw> buf[2];
+    std::future<bool> run[2];
+    auto start = [&](int s) {
         if (verbose > 1)
-            for (auto &z : cur) fprintf(stderr, "poa begin %s\n", z.hole.c_str());
-        const bool ok = run_chunk(cur, ctx, split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE);
+            for (auto &z : buf[s]) fprintf(stderr, "poa begin %s\n", z.hole.c_str());
+        run[s] = std::async(std::launch::async, [&, s]() {
+            const double t0 = now_ms();
+            const bool ok = run_chunk(buf[s], ctx[s % nslot], mode);
+            if (timing) fprintf(stderr, "[ccsx] chunk %zu ZMWs: GPU %.0f-%.0f ms\n", buf[s].size(), t0, now_ms());
+            return ok;
+        });
+    };
+    bool have = read_chunk(buf[0]);
+    if (have) start(0);
+    for (int s = 0; have; s ^= 1) {
+        // step 0 of chunk k + 1 overlaps chunk k on the GPUs; with two slots
+        // its launch does too
+        const int o = s ^ 1;
+        std::vector<Zmw>().swap(buf[o]);
+        bool next = false;
+        if (nslot == 2) {
+            next = read_chunk(buf[o]);
+            if (next) start(o);
+        } else {
+            std::future<bool> ahead = std::async(std::launch::async, [&]() { return read_chunk(buf[o]); });
+            const bool ok = run[s].get();
+            next = ahead.get();
+            if (next && ok) start(o);
+            run[s] = std::async(std::launch::deferred, [ok]() { return ok; });
+        }
+        const bool ok = run[s].get();
         if (ok) {
-            for (auto &z : cur) {
+            for (auto &z : buf[s]) {
                 if (verbose > 1) fprintf(stderr, "poa end %s\n", z.hole.c_str());
                 if (!z.ccs.empty()) fprintf(fp_out, ">%s/%s/ccs\n%s\n", z.movie.c_str(), z.hole.c_str(), z.ccs.c_str());
             }
         }
-        have = ahead.get();
         if (!ok) {
+            if (next && run[o].valid()) run[o].get();
             rc = 1;
             break;
         }
-        cur.swap(nxt);
+        have = next;
     }
-    for (auto *x : ctx) ccsx_gpu_close(x);
+    for (auto &v : ctx)
+        for (auto *x : v) ccsx_gpu_close(x);
     ccsx_reader_close(rd);
     if (fp_out != stdout) fclose(fp_out);
     else fflush(stdout);

@@ -23,7 +23,8 @@ MODE_PRIMITIVE = 1
 EXPORTS = {
     "ccsx_gpu.h": ["ccsx_gpu_device_count", "ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
-                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows"],
+                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows",
+                   "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw"],
     "ccsx_seqio.h": ["ccsx_reader_open", "ccsx_reader_next", "ccsx_reader_close"],

@@ -63,6 +63,16 @@ const char *ccsx_gpu_status_str(int32_t status);
  * (tight) workspace capacities is re-run with exact upper-bound capacities. */
 int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out);
 
+/* Contexts sharing one device concurrently (the CLI keeps two chunks in flight
+ * per GPU): cap this context's slices at total device memory / share
+ * (default 1 = whatever is free). */
+int ccsx_gpu_set_mem_share(ccsx_ctx *ctx, uint32_t share);
+/* on != 0: the first ccsx_gpu_run reserves the whole slice budget for the
+ * workspace at once instead of growing it with the chunk size (re-allocating
+ * a workspace a launch has touched costs ~30 ms per GB; a fresh one does
+ * not).  For long runs such as the CLI's growing chunks. */
+int ccsx_gpu_set_prealloc(ccsx_ctx *ctx, int on);
+
 /* The same in three steps (one slice, tight capacities, no re-run), so inputs
  * can stay resident in HBM across launches (used by bench.py).
  * ccsx_gpu_launch returns the kernel time measured with HIP events on the

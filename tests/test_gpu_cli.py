@@ -57,3 +57,20 @@ def test_cli_multi_chunk_order(tmp_path):
     got = open(out, "rb").read()
     assert got.count(b">") == 1100
     assert got == _expected(fa, 0)
+
+
+def test_cli_two_slots_match_one(tmp_path):
+    """Three chunks (1,024 + 4,096 + 180 ZMWs): with two chunk slots per GPU
+    chunk k + 1 runs on the device while chunk k drains; the output must be
+    byte-identical to one chunk in flight at a time, in input order."""
+    fa = str(tmp_path / "in.fa")
+    write(fa, 5300, 1000, 6)
+    outs = []
+    for slots in ("1", "2"):
+        out = str(tmp_path / f"out{slots}.fa")
+        r = subprocess.run([BIN, "-A", "-j", "8", fa, out], env=dict(os.environ, CCSX_SLOTS=slots),
+                           capture_output=True, timeout=300)
+        assert r.returncode == 0, r.stderr.decode()
+        outs.append(open(out, "rb").read())
+    assert outs[0].count(b">") == 5300
+    assert outs[0] == outs[1]

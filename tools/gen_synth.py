@@ -1,5 +1,6 @@
 """Write a synthetic subread FASTA: `synth/<hole>/<qs>_<qe>` names,
-single-line uppercase records.  Usage: gen_synth.py OUT.fa NZMW L PASSES [HOLE0]"""
+single-line uppercase records.  Usage: gen_synth.py OUT.fa NZMW L PASSES [HOLE0]
+(L = 0: per-hole insert length and passes of bench.py's config E)."""
 import os
 import sys
 
@@ -10,7 +11,11 @@ import ccsx_amd as cx  # noqa: E402
 def write(path, nzmw, L, passes, hole0=0, seed=20201104, movie="synth"):
     with open(path, "wb") as f:
         for h in range(hole0, hole0 + nzmw):
-            subs, _ = cx.synth_zmw(seed, h, L, passes)
+            if L:
+                subs, _ = cx.synth_zmw(seed, h, L, passes)
+            else:
+                from bench import CONFIGS, zmw_shape
+                subs, _ = cx.synth_zmw(seed, h, *zmw_shape(CONFIGS["E"], h))
             qs = 0
             for s in subs:
                 f.write(b">%s/%d/%d_%d\n%s\n" % (movie.encode(), h, qs, qs + len(s), s))
