@@ -22,6 +22,28 @@ extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, 
 
 namespace {
 
+// pinned host staging (grow-only): DMA straight from / to it, no pageable
+// bounce and no per-slice zero-fill of a fresh std::vector
+struct HostBuf {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t c = std::max<size_t>(n + n / 4, 4096);
+        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p), c, hipHostMallocDefault);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    ~HostBuf()
+    {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -80,7 +102,7 @@ struct ccsx_ctx {
     std::vector<unsigned long long> h_prof;
     DevBuf d_seq, d_soff, d_slen, d_desc, d_order, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
     // fetched results
-    std::vector<uint8_t> h_out;
+    HostBuf h_out, h_seq;
     std::vector<uint32_t> h_olen, h_ncols;
     std::vector<int32_t> h_status;
     std::vector<unsigned long long> h_cells;
@@ -252,7 +274,8 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, c->d_cells.reserve(nz * 8));
     const auto tb = std::chrono::steady_clock::now();
     // host staging of the sequence arena and segment tables
-    std::vector<uint8_t> hseq(seq_b);
+    HIPCHK(c, c->h_seq.reserve(seq_b));
+    uint8_t *hseq = c->h_seq.p;
     std::vector<uint32_t> hoff(nseg), hlen(nseg);
     for (size_t i = 0; i < nz; ++i) {
         const ccsx_zmw_in &zi = z[i];
@@ -263,9 +286,9 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
             hlen[d.seg0 + k] = zi.seg_len[k];
             hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
         }
-        if (hi) memcpy(hseq.data() + d.seq_off, zi.seqs, hi);
+        if (hi) memcpy(hseq + d.seq_off, zi.seqs, hi);
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_seq.p, hseq.data(), seq_b, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_seq.p, hseq, seq_b, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_soff.p, hoff.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_slen.p, hlen.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_desc.p, c->desc.data(), nz * sizeof(ccsx::ZmwDesc), hipMemcpyHostToDevice,
@@ -346,7 +369,7 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
     if (!c) return -1;
     HIPCHK(c, hipSetDevice(c->device));
     const size_t nz = c->nz;
-    c->h_out.resize(c->out_bytes);
+    HIPCHK(c, c->h_out.reserve(c->out_bytes));
     c->h_olen.resize(nz);
     c->h_status.resize(nz);
     c->h_cells.resize(nz);
@@ -354,12 +377,12 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
         HIPCHK(c, hipMemcpyAsync(c->h_olen.data(), c->d_olen.p, nz * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_status.data(), c->d_status.p, nz * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_cells.data(), c->d_cells.p, nz * 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_out.data(), c->d_out.p, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_out.p, c->d_out.p, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     int bad = 0;
     for (size_t i = 0; i < nz; ++i) {
-        out[i].ccs = reinterpret_cast<const char *>(c->h_out.data() + c->desc[i].out_off);
+        out[i].ccs = reinterpret_cast<const char *>(c->h_out.p + c->desc[i].out_off);
         out[i].len = c->h_status[i] ? 0 : c->h_olen[i];
         out[i].status = c->h_status[i];
         out[i].cells = c->h_cells[i];
