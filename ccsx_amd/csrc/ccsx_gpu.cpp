@@ -22,32 +22,49 @@ extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, 
 
 namespace {
 
-// pinned host staging (grow-only): DMA straight from / to it, no pageable
-// bounce and no per-slice zero-fill of a fresh std::vector
+// pinned host staging (grow-only): DMA straight from / to it,
+// no pageable bounce and no per-slice zero-fill of a fresh std::vector.  If
+// pinning fails (many contexts x slots each pinning ~1 GB arenas), the buffer
+// falls back to pageable memory: the copies then stage through the driver,
+// slower but correct.
 struct HostBuf {
     uint8_t *p = nullptr;
     size_t cap = 0;
+    bool pinned = false;
+    void release()
+    {
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else free(p);
+        }
+        p = nullptr;
+        cap = 0;
+        pinned = false;
+    }
     hipError_t reserve(size_t n)
     {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         const size_t c = std::max<size_t>(n + n / 4, 4096);
         hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p), c, hipHostMallocDefault);
-        if (e == hipSuccess) cap = c;
-        return e;
+        if (e == hipSuccess) {
+            pinned = true;
+        } else {
+            (void)hipGetLastError();
+            p = static_cast<uint8_t *>(malloc(c));
+            if (!p) return hipErrorOutOfMemory;
+        }
+        cap = c;
+        return hipSuccess;
     }
-    ~HostBuf()
-    {
-        if (p) (void)hipHostFree(p);
-    }
+    ~HostBuf() { release(); }
 };
 
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
-    hipError_t reserve(size_t n)
+    // exact: allocate exactly n (the CLI's one-off slice-budget reservation)
+    hipError_t reserve(size_t n, bool exact = false)
     {
         if (n <= cap) return hipSuccess;
         if (p) (void)hipFree(p);
@@ -57,7 +74,7 @@ struct DevBuf {
         // one chunk differ by a few percent, and re-allocating a workspace a
         // full launch has touched measured 1-5 s per 75-150 GB (DESIGN.md
         // section 7)
-        size_t c = std::max<size_t>(n + n / 4, 256);
+        size_t c = std::max<size_t>(exact ? n : n + n / 4, 256);
         hipError_t e = hipMalloc(&p, c);
         if (e != hipSuccess) {
             (void)hipGetLastError();
@@ -95,6 +112,7 @@ struct ccsx_ctx {
     std::vector<ccsx::ZmwDesc> desc;
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
+    int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
     bool prealloc = false;             // reserve the slice budget up front
     std::vector<uint8_t> run_arena;    // ccsx_gpu_run's gathered CCS strings
@@ -173,7 +191,7 @@ const char *ccsx_gpu_status_str(int32_t s)
     case ccsx::kErrEdges: return "graph edges exceed capacity";
     case ccsx::kErrMulti: return "multi-predecessor rows exceed capacity";
     case ccsx::kErrSpill: return "spilled DP rows exceed capacity";
-    case ccsx::kErrInDegree: return "node in-degree > 255";
+    case ccsx::kErrInDegree: return "far-row in-degree > 63";
     case ccsx::kErrReadLen: return "read longer than the LDS read buffer";
     case ccsx::kErrOut: return "consensus longer than the output slab";
     case ccsx::kErrTrace: return "traceback did not terminate";
@@ -414,7 +432,10 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     HIPCHK(c, hipSetDevice(c->device));
     size_t freeb = 0, totb = 0;
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
-    const uint64_t held = c->d_ws.cap + c->d_seq.cap + c->d_out.cap + c->d_msa.cap;
+    // the workspace may grow into what is free plus what it already holds;
+    // the sequence / output arenas it would need beside it stay counted as
+    // used (they are re-reserved per slice, not released)
+    const uint64_t held = c->d_ws.cap;
     uint64_t budget = freeb + held > (3ull << 30) ? freeb + held - (3ull << 30) : (1ull << 30);
     {
         // at most half the device per context (and a fixed share of it when
@@ -426,7 +447,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         const uint64_t part = totb / (2ull * c->mem_share);
         budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
     }
-    if (c->prealloc && c->d_ws.cap < budget) HIPCHK(c, c->d_ws.reserve(budget));
+    if (c->prealloc && c->d_ws.cap < budget) HIPCHK(c, c->d_ws.reserve(budget, true));
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     c->run_arena.clear();
     std::vector<uint64_t> aoff(nz, 0);
@@ -489,6 +510,12 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     int r = run_list(all, false, &retry);
     if (!r && !retry.empty()) r = run_list(retry, true, nullptr);
     if (r) return r;
+    if (c->fault >= 0 && (size_t)c->fault < nz) {
+        out[c->fault].status = ccsx::kErrTrace;
+        out[c->fault].len = 0;
+        if (first_err.empty()) first_err = "ZMW failed on the device: injected fault (test hook)";
+    }
+    c->fault = -1;
     for (size_t i = 0; i < nz; ++i) out[i].ccs = reinterpret_cast<const char *>(c->run_arena.data() + aoff[i]);
     if (!first_err.empty()) {
         c->err = first_err;
@@ -501,6 +528,13 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *c, uint32_t rows)
 {
     if (!c) return -1;
     c->tight_rows = rows;
+    return 0;
+}
+
+int ccsx_gpu_set_fault(ccsx_ctx *c, int64_t zmw)
+{
+    if (!c) return -1;
+    c->fault = zmw;
     return 0;
 }
 

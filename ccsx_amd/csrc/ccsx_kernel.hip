@@ -310,6 +310,13 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
 //    always below the H' it extends);
 //  * free-end candidates are tracked on H' for the same reason.
 // ----------------------------------------------------------------------------
+// Cell records (16 bits, cell t of row r) sit in the row's 256 B at byte
+// (2 t + tb_rot(r)) & 255: each row is rotated by two words per row of its
+// 32-row traceback block, so the traceback's window fill -- 32 lanes reading
+// the same column of 32 consecutive rows -- spreads over the LDS banks instead
+// of hitting one (a 256 B pitch is a multiple of the 32-bank width).
+__device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; }
+
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
 constexpr int kBlkAB = 4;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2
@@ -940,7 +947,9 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     }
     if (e0 > S.bE) S.bE = e0, S.bKey = r * 2, S.bOff = off;
     if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1, S.bOff = off;
-    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), S.rc, r * 256u + (uint32_t)lane * 4u, 0, 0);
+    // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
+    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), S.rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
+                                          0);
     DP_STAMP(kPfFlush);
 }
 
@@ -1177,24 +1186,27 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
     uint32_t r = er, bi = er / kTbRows, buf = 0, base = bi * kTbRows;
     int32_t j = (int32_t)ej;
-    // per staged block: lane l < 32 holds the LDS byte address of row
-    // base + l's record for read position 0 (so cell (r, j) sits at
-    // vrow[r - base] + 2 j), farm the block's far rows (tags are slots)
-    uint32_t vrow = 0, farm = 0;
+    // per staged block, lane l < 32 = block row l: voff = its band offset,
+    // vrot = (tb_rot - 2 off) & 255, so cell (r, j) sits at byte
+    // ((buf * 32 + l) << 8) | ((vrot + 2 j) & 255) of the LDS; farm = the
+    // block's far rows (tags are slots)
+    uint32_t voff = 0, vrot = 0, farm = 0;
 #ifndef CCSX_TB_NOWIN
     // record window of the plain MPRED steps: lane l holds the records of
     // block row l & 31 at columns jw - 1 - 2 (l >> 5) (low half) and the
     // column below it (high half), i.e. four columns of every staged row;
     // valid while j lies in [jw - 4, jw) (entering a block invalidates it)
-    uint32_t vrow32 = 0, win = 0;
+    uint32_t vrot32 = 0, rowb32 = 0, win = 0;
     int32_t jw = INT32_MIN / 2;
 #endif
     auto enter = [&]() {
         const uint32_t mt = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
-        vrow = buf * (kTbBufWords * 4u) + lane * 256u - 2u * (mt & 0x7FFFFFFFu);
+        voff = mt & 0x7FFFFFFFu;
+        vrot = (tb_rot(lane) - 2u * voff) & 255u;
         farm = (uint32_t)ballot((mt >> 31) != 0u);
 #ifndef CCSX_TB_NOWIN
-        vrow32 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & 31u) * 4u), (int)vrow) - ((lane >> 5) * 4u);
+        vrot32 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & 31u) * 4u), (int)vrot) - ((lane >> 5) * 4u);
+        rowb32 = (buf * 32u + (lane & 31u)) << 8;
         jw = INT32_MIN / 2;
 #endif
     };
@@ -1251,7 +1263,9 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     };
     // the record of cell (r, j); r must lie in the staged block
     auto rec_at = [&]() -> uint32_t {
-        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)vrow, (int)(r - base)) + 2u * (uint32_t)j;
+        const uint32_t li = r - base;
+        const uint32_t a = ((buf * 32u + li) << 8) |
+                           (((uint32_t)__builtin_amdgcn_readlane((int)vrot, (int)li) + 2u * (uint32_t)j) & 255u);
         return uni((uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + a));
     };
     auto cell = [&]() -> uint32_t {
@@ -1313,9 +1327,9 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 // every fourth column
                 uint32_t k = (uint32_t)(jw - 1 - j);
                 if (k >= 4u) {
-                    const uint32_t a = vrow32 + 2u * (uint32_t)j;
-                    const uint32_t lo = *reinterpret_cast<const uint16_t *>(lds8 + a);
-                    const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds8 + a - 2u);
+                    const uint32_t a = vrot32 + 2u * (uint32_t)j;
+                    const uint32_t lo = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | (a & 255u)));
+                    const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | ((a - 2u) & 255u)));
                     win = lo | hi << 16;
                     jw = j + 1, k = 0;
                 }
@@ -1333,10 +1347,11 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 const int32_t i = (int32_t)lane;
                 const int32_t ri = (int32_t)(r - base) - 1 - i, ji = j - 1 - i;
                 const bool in = ri >= 0 && (ji & ~63) == chunk;
-                const uint32_t rb = (uint32_t)__builtin_amdgcn_ds_bpermute((in ? ri : 0) * 4, (int)vrow);
-                const uint32_t ti = (rb + 2u * (uint32_t)ji - (buf * (kTbBufWords * 4u) + (uint32_t)ri * 256u)) >> 1;
+                const uint32_t oi = (uint32_t)__builtin_amdgcn_ds_bpermute((in ? ri : 0) * 4, (int)voff);
+                const uint32_t ti = (uint32_t)ji - oi;
                 const bool inb = in && ti < (uint32_t)kW;
-                const uint32_t rc = inb ? (uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + rb + 2u * (uint32_t)ji) : 0u;
+                const uint32_t ab = ((buf * 32u + (uint32_t)ri) << 8) | ((2u * ti + tb_rot((uint32_t)ri)) & 255u);
+                const uint32_t rc = inb ? (uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + ab) : 0u;
                 const bool ok = inb && !((farm >> (uint32_t)(in ? ri : 0)) & 1u) && (rc & 0x3F3u) == 0x10u;
                 const uint64_t bad = ~ballot(ok);
                 const uint32_t k = (uint32_t)__builtin_ctzll(bad);  // cells r-1 .. r-k continue the run (k < 64)

@@ -2,19 +2,33 @@
 // MI355X engine.
 //
 // Restates main.c:723-870 (options, I/O, chunked pipeline) and step 0 / step 2
-// of worker_pipeline (main.c:649-720).  Step 1 -- kt_for(ccs_for2/ccs_for) --
-// becomes: ccs_prepare + strand flip on -j CPU threads, then one batched
-// device call per GPU (include/ccsx_gpu.h), the chunk's ZMWs split across the
-// visible GPUs in contiguous ranges and gathered back in input order.
+// of worker_pipeline (main.c:649-720).  Step 1 -- kt_for(ccs_for2/ccs_for),
+// which deals the chunk's ZMWs over CPU threads with work stealing
+// (kthread.c:24-46) -- becomes:
+//   * ccs_prepare + strand flip on -j CPU threads (main.c:520-536);
+//   * the chunk's ZMWs cut into cost-balanced micro-batches in
+//     longest-first order (host/dispatch.cpp), queued behind the previous
+//     chunk's;
+//   * one worker thread per device context pulls batches from the queue and
+//     runs them through the batched C-ABI (include/ccsx_gpu.h); two contexts
+//     per GPU by default, so one stages and fetches while the other's kernel
+//     runs and the tail of one launch overlaps the next;
+//   * a writer thread emits each chunk in input order once its last batch is
+//     back (main.c:707-717).
+// A ZMW the device cannot finish is reported on stderr and skipped; the other
+// ZMWs of the run are written (the reference has no per-ZMW failure).
 #include <getopt.h>
 
 #include <algorithm>
-#include <chrono>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <future>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_set>
@@ -30,7 +44,20 @@ struct Zmw {
     std::string movie, hole, seqs;
     std::vector<uint32_t> lens;
     std::vector<uint32_t> seg_off, seg_len;
+    std::vector<uint8_t> seg_rev;
     std::string ccs;
+    int32_t status = 0;
+};
+
+struct Chunk {
+    size_t id = 0;
+    std::vector<Zmw> zs;
+    std::atomic<size_t> pending{0};  // batches not yet back from a device
+};
+
+struct Batch {
+    std::shared_ptr<Chunk> chunk;
+    std::vector<uint32_t> idx;  // ZMWs of the chunk
 };
 
 int usage()
@@ -53,7 +80,10 @@ int usage()
             "-j     <int>   Number of CPU threads for subread preparation. [1] \n"
             "\n"
             "Environment:\n"
-            "CCSX_NGPU      Number of GPUs to use [all visible]\n"
+            "CCSX_NGPU      Number of GPU contexts groups [all visible GPUs]; more than the visible\n"
+            "               GPUs places group g on GPU g %% visible (logical contexts)\n"
+            "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
+            "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
             "\n"
             "Arguments:\n"
             "input          Input file.\n"
@@ -63,23 +93,38 @@ int usage()
 }
 
 // ccs_prepare + strand flip for every ZMW of the chunk on nthreads threads
-// (the CPU half of step 1, main.c:520-536)
+// (the CPU half of step 1, main.c:520-536, with its -v output)
 void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
 {
     std::atomic<size_t> next(0);
     auto work = [&]() {
+        std::string msg;
         for (size_t i; (i = next.fetch_add(1)) < zs.size();) {
             Zmw &z = zs[i];
             const uint32_t n = (uint32_t)z.lens.size();
             z.seg_off.resize(n);
             z.seg_len.resize(n);
-            const uint32_t ns = ccsx_prepare_apply(&z.seqs[0], z.lens.data(), n, z.seg_off.data(), z.seg_len.data());
+            z.seg_rev.resize(n);
+            const uint32_t ns = ccsx_prepare(&z.seqs[0], z.lens.data(), n, z.seg_off.data(), z.seg_len.data(),
+                                             z.seg_rev.data());
             z.seg_off.resize(ns);
             z.seg_len.resize(ns);
-            if (verbose)
-                for (uint32_t l = 0; l < ns; ++l)
-                    fprintf(stderr, ">%s_%u/%u len=%u \n%.*s\n", z.hole.c_str(), l, ns, z.seg_len[l], (int)z.seg_len[l],
-                            z.seqs.data() + z.seg_off[l]);
+            z.seg_rev.resize(ns);
+            msg.clear();
+            if (verbose > 1) msg += "poa begin " + z.hole + "\n";
+            for (uint32_t l = 0; l < ns; ++l) {
+                if (z.seg_rev[l]) ccsx_revcomp(&z.seqs[z.seg_off[l]], z.seg_len[l]);
+                if (verbose) {
+                    // main.c:477-479 / 533-535
+                    char h[160];
+                    snprintf(h, sizeof h, ">%s_%u/%u strand=%d len=%u \n", z.hole.c_str(), l, ns, z.seg_rev[l],
+                             z.seg_len[l]);
+                    msg += h;
+                    msg.append(z.seqs, z.seg_off[l], z.seg_len[l]);
+                    msg += '\n';
+                }
+            }
+            if (!msg.empty()) fwrite(msg.data(), 1, msg.size(), stderr);
         }
     };
     std::vector<std::thread> th;
@@ -88,32 +133,101 @@ void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
     for (auto &t : th) t.join();
 }
 
-// the GPU half of step 1: contiguous ranges of the chunk per device
-bool run_chunk(std::vector<Zmw> &zs, std::vector<ccsx_ctx *> &ctx, int mode)
-{
-    const size_t ng = ctx.size(), nz = zs.size();
-    std::vector<std::thread> th;
-    std::atomic<bool> ok(true);
-    for (size_t g = 0; g < ng; ++g) {
-        const size_t b = nz * g / ng, e = nz * (g + 1) / ng;
-        th.emplace_back([&, g, b, e]() {
-            if (b == e) return;
-            std::vector<ccsx_zmw_in> in(e - b);
-            std::vector<ccsx_zmw_out> out(e - b);
-            for (size_t i = b; i < e; ++i)
-                in[i - b] = ccsx_zmw_in{zs[i].seqs.data(), zs[i].seg_off.data(), zs[i].seg_len.data(),
-                                        (uint32_t)zs[i].seg_len.size()};
-            if (ccsx_gpu_run(ctx[g], mode, in.data(), in.size(), out.data()) != 0) {
-                fprintf(stderr, "[ccsx] GPU %zu: %s\n", g, ccsx_gpu_error(ctx[g]));
-                ok = false;
-                return;
-            }
-            for (size_t i = b; i < e; ++i) zs[i].ccs.assign(out[i - b].ccs, out[i - b].len);
-        });
+// the batch queue between step 0 and the device workers
+class BatchQueue {
+public:
+    void push(std::vector<Batch> &&bs)
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            for (auto &b : bs) q_.push_back(std::move(b));
+        }
+        cv_.notify_all();
     }
-    for (auto &t : th) t.join();
-    return ok;
-}
+    void close()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            closed_ = true;
+        }
+        cv_.notify_all();
+    }
+    bool pop(Batch &b)
+    {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [this] { return closed_ || !q_.empty(); });
+        if (q_.empty()) return false;
+        b = std::move(q_.front());
+        q_.pop_front();
+        return true;
+    }
+
+private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<Batch> q_;
+    bool closed_ = false;
+};
+
+// chunks in input order, handed from step 0 to the writer; bounded so step 0
+// runs at most `limit` chunks ahead of the output
+class ChunkRing {
+public:
+    explicit ChunkRing(size_t limit) : limit_(limit) {}
+    void add(const std::shared_ptr<Chunk> &c)
+    {
+        std::unique_lock<std::mutex> g(m_);
+        space_.wait(g, [this] { return q_.size() < limit_ || stop_; });
+        q_.push_back(c);
+        ready_.notify_all();
+    }
+    void finish()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            eof_ = true;
+        }
+        ready_.notify_all();
+    }
+    void stop()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        space_.notify_all();
+        ready_.notify_all();
+    }
+    void batch_done()
+    {
+        // the decrement happened outside the lock: take it once so a writer
+        // between its predicate check and its wait cannot miss this wake-up
+        { std::lock_guard<std::mutex> g(m_); }
+        ready_.notify_all();
+    }
+    // the oldest chunk once every batch of it is back; null at the end
+    std::shared_ptr<Chunk> next_done()
+    {
+        std::unique_lock<std::mutex> g(m_);
+        ready_.wait(g, [this] { return stop_ || (!q_.empty() && q_.front()->pending == 0) || (q_.empty() && eof_); });
+        if (stop_ || q_.empty()) return nullptr;
+        auto c = q_.front();
+        return c;
+    }
+    void pop()
+    {
+        std::lock_guard<std::mutex> g(m_);
+        q_.pop_front();
+        space_.notify_all();
+    }
+
+private:
+    std::mutex m_;
+    std::condition_variable space_, ready_;
+    std::deque<std::shared_ptr<Chunk>> q_;
+    size_t limit_;
+    bool eof_ = false, stop_ = false;
+};
 
 }  // namespace
 
@@ -177,41 +291,116 @@ int main(int argc, char **argv)
         fprintf(stderr, "Cannot open file for write!\n");
         return 1;
     }
-    int ndev = ccsx_gpu_device_count();
+    const int ndev = ccsx_gpu_device_count();
     if (ndev <= 0) {
         fprintf(stderr, "[ccsx] no HIP device: the MI355X engine needs a GPU\n");
         return 1;
     }
-    if (const char *e = getenv("CCSX_NGPU")) ndev = std::max(1, std::min(ndev, atoi(e)));
-    // CCSX_SLOTS=2: two chunk slots per GPU, each with its own context and
-    // stream, chunk k + 1 launched on the other slot while chunk k drains (so
-    // the CUs its finished workgroups free could take chunk k + 1's work).
-    // Measured slower on MI355X (the concurrent chunk's
-    // staging stalls the running one), so one chunk in flight is the default;
-    // with one slot, chunk k + 1 is launched before chunk k is written out.
-    int nslot = 1;
-    if (const char *e = getenv("CCSX_SLOTS")) nslot = std::max(1, std::min(2, atoi(e)));
-    std::vector<std::vector<ccsx_ctx *>> ctx(nslot, std::vector<ccsx_ctx *>(ndev, nullptr));
-    for (int s = 0; s < nslot; ++s)
-        for (int g = 0; g < ndev; ++g) {
-            if (ccsx_gpu_open(g, &ctx[s][g]) != 0) return 1;
-            ccsx_gpu_set_mem_share(ctx[s][g], (uint32_t)nslot);
-            ccsx_gpu_set_prealloc(ctx[s][g], 1);
-        }
+    // CCSX_NGPU groups of CCSX_SLOTS contexts; group g on device g % ndev
+    // (more groups than devices: logical contexts sharing a device, which is
+    // how the multi-GPU split is exercised on a one-GPU box)
+    int ngroup = ndev, nslot = 2;
+    if (const char *e = getenv("CCSX_NGPU")) ngroup = std::max(1, std::min(64, atoi(e)));
+    if (const char *e = getenv("CCSX_SLOTS")) nslot = std::max(1, std::min(8, atoi(e)));
+    const int nctx = ngroup * nslot;
+    std::vector<ccsx_ctx *> ctx(nctx, nullptr);
+    std::vector<int> per_dev(ndev, 0);
+    for (int i = 0; i < nctx; ++i) per_dev[(i / nslot) % ndev]++;
+    for (int i = 0; i < nctx; ++i) {
+        const int dev = (i / nslot) % ndev;
+        if (ccsx_gpu_open(dev, &ctx[i]) != 0) return 1;
+        ccsx_gpu_set_mem_share(ctx[i], (uint32_t)per_dev[dev]);
+        ccsx_gpu_set_prealloc(ctx[i], 1);
+    }
     if (nthreads < 1) nthreads = 1;
 
-    // main.c:652-697 (step 0), 698-706 (step 1), 707-717 (step 2).  As the
-    // reference's kt_pipeline overlaps step 0 of the next chunk with step 1,
-    // chunk k + 1 is read and prepared on the CPU while the GPUs run chunk k;
-    // chunks are written in input order.
-    size_t chunk_size = 1024;
-    // CCSX_TIMING=1: per-chunk wall-clock phases on stderr (ms since start)
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     const auto tstart = std::chrono::steady_clock::now();
     auto now_ms = [tstart]() {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tstart).count();
     };
-    auto read_chunk = [&](std::vector<Zmw> &zs) -> bool {
+    const int mode = split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE;
+
+    BatchQueue queue;
+    ChunkRing ring(3);
+    std::atomic<bool> fatal(false);
+    std::mutex err_m;
+
+    // test hook: the device reports this hole as failed (tests/test_gpu_cli.py)
+    const std::string fault_hole = getenv("CCSX_FAULT_HOLE") ? getenv("CCSX_FAULT_HOLE") : "";
+
+    // step 1, device side: one worker per context
+    auto worker = [&](int w) {
+        Batch b;
+        std::vector<ccsx_zmw_in> in;
+        std::vector<ccsx_zmw_out> out;
+        while (queue.pop(b)) {
+            Chunk &ch = *b.chunk;
+            if (!fatal) {
+                in.resize(b.idx.size());
+                out.assign(b.idx.size(), ccsx_zmw_out{});
+                for (size_t i = 0; i < b.idx.size(); ++i) {
+                    const Zmw &z = ch.zs[b.idx[i]];
+                    in[i] = ccsx_zmw_in{z.seqs.data(), z.seg_off.data(), z.seg_len.data(), (uint32_t)z.seg_len.size()};
+                    if (!fault_hole.empty() && z.hole == fault_hole) ccsx_gpu_set_fault(ctx[w], (int64_t)i);
+                }
+                const double t0 = now_ms();
+                const int r = ccsx_gpu_run(ctx[w], mode, in.data(), in.size(), out.data());
+                if (r == 0 || r == -2) {
+                    // -2: some ZMWs failed on the device, the rest are valid
+                    for (size_t i = 0; i < b.idx.size(); ++i) {
+                        Zmw &z = ch.zs[b.idx[i]];
+                        z.status = out[i].status;
+                        if (!out[i].status) z.ccs.assign(out[i].ccs, out[i].len);
+                    }
+                } else {
+                    std::lock_guard<std::mutex> g(err_m);
+                    fprintf(stderr, "[ccsx] device context %d: %s\n", w, ccsx_gpu_error(ctx[w]));
+                    fatal = true;
+                }
+                if (timing)
+                    fprintf(stderr, "[ccsx] chunk %zu batch of %zu ZMWs on context %d: %.0f-%.0f ms\n", ch.id,
+                            b.idx.size(), w, t0, now_ms());
+            }
+            b.chunk->pending.fetch_sub(1);
+            ring.batch_done();
+            b.chunk.reset();
+        }
+    };
+    std::vector<std::thread> workers;
+    for (int w = 0; w < nctx; ++w) workers.emplace_back(worker, w);
+
+    // step 2: ordered output (main.c:707-717)
+    size_t nfail = 0;
+    std::thread writer([&]() {
+        while (auto ch = ring.next_done()) {
+            if (!fatal) {
+                for (auto &z : ch->zs) {
+                    if (z.status) {
+                        ++nfail;
+                        fprintf(stderr, "[ccsx] %s/%s: no CCS, the device could not finish this ZMW (%s)\n",
+                                z.movie.c_str(), z.hole.c_str(), ccsx_gpu_status_str(z.status));
+                        continue;
+                    }
+                    if (verbose > 1) fprintf(stderr, "poa end %s\n", z.hole.c_str());
+                    if (!z.ccs.empty())
+                        fprintf(fp_out, ">%s/%s/ccs\n%s\n", z.movie.c_str(), z.hole.c_str(), z.ccs.c_str());
+                }
+            }
+            if (timing) fprintf(stderr, "[ccsx] chunk %zu written at %.0f ms\n", ch->id, now_ms());
+            ring.pop();
+        }
+    });
+
+    // step 0 (main.c:652-697) + the CPU half of step 1; the reference grows
+    // the chunk 1,024 -> 4,096 -> 16,384 ZMWs (main.c:686-690), here the
+    // last size scales with the devices (output order does not depend on it)
+    const size_t chunk_max = 16384u * (size_t)std::min(ngroup, 4);
+    size_t chunk_size = 1024;
+    for (size_t id = 0; !fatal; ++id) {
+        auto ch = std::make_shared<Chunk>();
+        ch->id = id;
+        std::vector<Zmw> &zs = ch->zs;
         const double t0 = now_ms();
         const char *movie, *hole, *seqs;
         const uint32_t *lens;
@@ -222,77 +411,49 @@ int main(int argc, char **argv)
             for (int i = 0; i < l; ++i) total += lens[i];
             if (total > (size_t)max_subread_len || total < (size_t)min_subread_len) continue;
             if (have_holes && hole_set.count(hole)) continue;
-            Zmw z;
+            zs.emplace_back();
+            Zmw &z = zs.back();
             z.movie = movie, z.hole = hole;
             z.seqs.assign(seqs, total);
             z.lens.assign(lens, lens + l);
-            zs.push_back(std::move(z));
             if (zs.size() >= chunk_size) {
-                if (chunk_size < 16384) chunk_size *= 4;
+                chunk_size = std::min(chunk_size * 4, chunk_max);
                 break;
             }
         }
         // kt_pipeline stops on an empty chunk (main.c:694-697); a chunk cut
         // short by -1 (end of input or an invalid name) is processed and the
-        // next call reads on, as the reference's next step 0 does
-        if (zs.empty()) return false;
+        // next read goes on, as the reference's next step 0 does
+        if (zs.empty()) break;
         const double t1 = now_ms();
         prepare_chunk(zs, nthreads, verbose);
+        // cost-balanced micro-batches, longest first (dispatch.cpp)
+        const uint32_t n = (uint32_t)zs.size();
+        std::vector<uint64_t> cost(n);
+        for (uint32_t i = 0; i < n; ++i) cost[i] = ccsx_zmw_cost(zs[i].seg_len.data(), (uint32_t)zs[i].seg_len.size());
+        std::vector<uint32_t> order(n), bounds(n + 1);
+        const uint32_t nb = ccsx_partition(cost.data(), n, (uint32_t)nctx * 2u, 256u, order.data(), bounds.data());
+        std::vector<Batch> bs(nb);
+        for (uint32_t b = 0; b < nb; ++b) {
+            bs[b].chunk = ch;
+            bs[b].idx.assign(order.begin() + bounds[b], order.begin() + bounds[b + 1]);
+        }
+        ch->pending = nb;
         if (timing)
-            fprintf(stderr, "[ccsx] chunk %zu ZMWs: read %.0f-%.0f ms, prepare until %.0f ms\n", zs.size(), t0, t1,
-                    now_ms());
-        return true;
-    };
-    int rc = 0;
-    const int mode = split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE;
-    std::vector<Zmw> buf[2];
-    std::future<bool> run[2];
-    auto start = [&](int s) {
-        if (verbose > 1)
-            for (auto &z : buf[s]) fprintf(stderr, "poa begin %s\n", z.hole.c_str());
-        run[s] = std::async(std::launch::async, [&, s]() {
-            const double t0 = now_ms();
-            const bool ok = run_chunk(buf[s], ctx[s % nslot], mode);
-            if (timing) fprintf(stderr, "[ccsx] chunk %zu ZMWs: GPU %.0f-%.0f ms\n", buf[s].size(), t0, now_ms());
-            return ok;
-        });
-    };
-    bool have = read_chunk(buf[0]);
-    if (have) start(0);
-    for (int s = 0; have; s ^= 1) {
-        // step 0 of chunk k + 1 overlaps chunk k on the GPUs; with two slots
-        // its launch does too
-        const int o = s ^ 1;
-        std::vector<Zmw>().swap(buf[o]);
-        bool next = false;
-        if (nslot == 2) {
-            next = read_chunk(buf[o]);
-            if (next) start(o);
-        } else {
-            std::future<bool> ahead = std::async(std::launch::async, [&]() { return read_chunk(buf[o]); });
-            const bool ok = run[s].get();
-            next = ahead.get();
-            if (next && ok) start(o);
-            run[s] = std::async(std::launch::deferred, [ok]() { return ok; });
-        }
-        const bool ok = run[s].get();
-        if (ok) {
-            for (auto &z : buf[s]) {
-                if (verbose > 1) fprintf(stderr, "poa end %s\n", z.hole.c_str());
-                if (!z.ccs.empty()) fprintf(fp_out, ">%s/%s/ccs\n%s\n", z.movie.c_str(), z.hole.c_str(), z.ccs.c_str());
-            }
-        }
-        if (!ok) {
-            if (next && run[o].valid()) run[o].get();
-            rc = 1;
-            break;
-        }
-        have = next;
+            fprintf(stderr, "[ccsx] chunk %zu: %u ZMWs read %.0f-%.0f ms, prepared until %.0f ms, %u batches\n", id, n,
+                    t0, t1, now_ms(), nb);
+        ring.add(ch);  // blocks while 3 chunks are ahead of the writer
+        queue.push(std::move(bs));
     }
-    for (auto &v : ctx)
-        for (auto *x : v) ccsx_gpu_close(x);
+    ring.finish();
+    queue.close();
+    for (auto &t : workers) t.join();
+    if (fatal) ring.stop();
+    writer.join();
+    for (auto *x : ctx) ccsx_gpu_close(x);
     ccsx_reader_close(rd);
     if (fp_out != stdout) fclose(fp_out);
     else fflush(stdout);
-    return rc;
+    if (nfail) fprintf(stderr, "[ccsx] %zu ZMWs had no CCS (device status, see above)\n", nfail);
+    return fatal ? 1 : 0;
 }

@@ -24,9 +24,10 @@ EXPORTS = {
     "ccsx_gpu.h": ["ccsx_gpu_device_count", "ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
                    "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows",
-                   "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc"],
+                   "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
-    "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw"],
+    "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
+                    "ccsx_zmw_cost", "ccsx_partition"],
     "ccsx_seqio.h": ["ccsx_reader_open", "ccsx_reader_next", "ccsx_reader_close"],
 }
 
@@ -82,6 +83,11 @@ def lib() -> C.CDLL:
         L.ccsx_synth_zmw.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_char_p,
                                      C.POINTER(C.c_uint32), C.c_char_p]
         L.ccsx_synth_zmw.restype = C.c_uint64
+        L.ccsx_zmw_cost.argtypes = [C.POINTER(C.c_uint32), C.c_uint32]
+        L.ccsx_zmw_cost.restype = C.c_uint64
+        L.ccsx_partition.argtypes = [C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ccsx_partition.restype = C.c_uint32
         L.ccsx_reader_open.argtypes = [C.c_char_p, C.c_int]
         L.ccsx_reader_open.restype = C.c_void_p
         L.ccsx_reader_next.argtypes = [C.c_void_p] + [C.POINTER(C.c_char_p)] * 2 + [C.POINTER(C.c_void_p),
@@ -151,6 +157,22 @@ def prepare_segments(subreads: list[bytes]):
     rv = np.zeros(max(n, 1), dtype=np.uint8)
     ns = lib().ccsx_prepare(seqs, _p32(lens), n, _p32(so), _p32(sl), rv.ctypes.data_as(C.POINTER(C.c_uint8)))
     return so[:ns].copy(), sl[:ns].copy(), rv[:ns].copy()
+
+
+def zmw_cost(seg_len) -> int:
+    """ccsx_zmw_cost: estimated POA work of a prepared ZMW (host/dispatch.cpp)."""
+    a = _u32(seg_len)
+    return int(lib().ccsx_zmw_cost(_p32(a), len(a)))
+
+
+def partition(costs, nparts: int, min_batch: int):
+    """ccsx_partition: (LPT order, list of batches as index lists into the input)."""
+    c = np.ascontiguousarray(np.asarray(costs, dtype=np.uint64))
+    n = len(c)
+    order = np.zeros(max(n, 1), dtype=np.uint32)
+    bounds = np.zeros(n + 1, dtype=np.uint32)
+    nb = lib().ccsx_partition(c.ctypes.data_as(C.POINTER(C.c_uint64)), n, nparts, min_batch, _p32(order), _p32(bounds))
+    return order[:n].tolist(), [order[bounds[b]:bounds[b + 1]].tolist() for b in range(nb)]
 
 
 def pairwise(q: bytes, t: bytes) -> dict:

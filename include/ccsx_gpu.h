@@ -18,8 +18,11 @@
  * call.  Output CCS strings live in a context-owned arena, valid until the
  * next ccsx_gpu_run / ccsx_gpu_fetch on the same context.
  * Errors: every function returns 0 on success, < 0 on error; the message is
- * ccsx_gpu_error(ctx).  The reference has no recoverable errors, so callers
- * treat any error as fatal.
+ * ccsx_gpu_error(ctx).  -1 is a context error (allocation, launch): the
+ * context's results are void.  ccsx_gpu_run / ccsx_gpu_fetch return -2 when
+ * individual ZMWs failed on the device (out[i].status != 0, no CCS); every
+ * other ZMW of the call is valid, and the host program skips only the failed
+ * ones (the reference has no per-ZMW failure to mirror).
  * Threading: one context per device; a context is used by one host thread.
  */
 #ifndef CCSX_GPU_H
@@ -60,7 +63,8 @@ const char *ccsx_gpu_status_str(int32_t status);
 
 /* One chunk (replaces kt_for(ccs_for2/ccs_for)): stage + launch + fetch, in
  * slices that fit the device memory; a ZMW whose graph outgrows the default
- * (tight) workspace capacities is re-run with exact upper-bound capacities. */
+ * (tight) workspace capacities is re-run with exact upper-bound capacities.
+ * Returns 0, -2 (some ZMWs failed, see out[i].status) or -1. */
 int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out);
 
 /* Contexts sharing one device concurrently (the CLI keeps two chunks in flight
@@ -90,6 +94,10 @@ uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *ctx);
 int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
 /* Test hook: tight row capacity override (0 = default 3 x longest segment + 4096). */
 int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
+/* Test hook: the next ccsx_gpu_run reports ZMW `zmw` (index into its batch)
+ * as failed (status 8) after computing it, as a device failure would; the
+ * run returns -2 and the other ZMWs are valid.  -1 = off. */
+int ccsx_gpu_set_fault(ccsx_ctx *ctx, int64_t zmw);
 int ccsx_gpu_profile(ccsx_ctx *ctx, uint64_t *sums, uint32_t nslots);
 /* Diagnostics: the same counters per ZMW (staging order), nslots per ZMW;
  * out holds nzmw * nslots values. */

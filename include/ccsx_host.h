@@ -38,6 +38,19 @@ typedef struct {
 } ccsx_pairaln;
 ccsx_pairaln ccsx_pairwise(const uint8_t *q, uint32_t qlen, const uint8_t *t, uint32_t tlen);
 
+/* Multi-GPU step 1 of the host program (replaces kt_for's dynamic dealing of
+ * ZMW indices over threads, kthread.c:24-46).
+ * ccsx_zmw_cost: estimated POA work of one prepared ZMW, S x (28 + nseg) with
+ * S = sum of segment lengths.
+ * ccsx_partition: order[n] = the ZMWs by decreasing cost (ties in input
+ * order); bounds[0..nb] = batch b is order[bounds[b] .. bounds[b+1]).  Batches
+ * are consecutive runs of about total / nparts cost, none (except a lone one)
+ * below min_batch ZMWs.  bounds needs room for n + 1 entries (nb <= n).
+ * Returns nb. */
+uint64_t ccsx_zmw_cost(const uint32_t *seg_len, uint32_t nseg);
+uint32_t ccsx_partition(const uint64_t *cost, uint32_t n, uint32_t nparts, uint32_t min_batch,
+                        uint32_t *order, uint32_t *bounds);
+
 /* Synthetic PacBio-like ZMW: insert of length L drawn from
  * splitmix64(seed ^ hole), `passes` full passes on alternating strands with
  * 6% insertions / 3% deletions / 1% substitutions.  Writes the concatenated

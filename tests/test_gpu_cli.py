@@ -7,24 +7,28 @@ import subprocess
 import pytest
 
 import ccsx_amd as cx
-from oracle.oracle import Poa
-from tools.gen_synth import write
+from oracle.oracle import batch
+from tools.gen_synth import records, write, write_bam
 
 pytestmark = pytest.mark.gpu
 BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ccsx_amd", "bin", "ccsx")
 
 
-def _expected(path, mode, min_count=3, mn=5000, mx=500000, exclude=()):
-    out = []
-    g = Poa()
-    for movie, hole, subs in cx.read_zmws(path):
+def _expected(path, mode, min_count=3, mn=5000, mx=500000, exclude=(), is_bam=False):
+    """The oracle on the same records, filters and push lists as the CLI."""
+    keep = []
+    for movie, hole, subs in cx.read_zmws(path, is_bam):
         if len(subs) < min_count + 2 or not (mn <= sum(map(len, subs)) <= mx) or hole in exclude:
             continue
-        p = cx.prepare(subs)
-        ccs = g.zmw(p.seqs, p.offs, p.lens, mode)
-        if ccs:
-            out.append(b">%s/%s/ccs\n%s\n" % (movie.encode(), hole.encode(), ccs))
-    return b"".join(out)
+        keep.append((movie, hole, cx.prepare(subs)))
+    ccs, _, _ = batch([p for _, _, p in keep], mode, 16)
+    return b"".join(b">%s/%s/ccs\n%s\n" % (m.encode(), h.encode(), c) for (m, h, _), c in zip(keep, ccs) if c)
+
+
+def _run(args, env=None, timeout=300):
+    r = subprocess.run([BIN] + args, capture_output=True, timeout=timeout, env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    return r
 
 
 @pytest.mark.parametrize("mode_flag,mode", [([], 0), (["-P"], 1)])
@@ -59,18 +63,57 @@ def test_cli_multi_chunk_order(tmp_path):
     assert got == _expected(fa, 0)
 
 
-def test_cli_two_slots_match_one(tmp_path):
-    """Three chunks (1,024 + 4,096 + 180 ZMWs): with two chunk slots per GPU
-    chunk k + 1 runs on the device while chunk k drains; the output must be
-    byte-identical to one chunk in flight at a time, in input order."""
+def test_cli_logical_contexts_match_one(tmp_path):
+    """Three chunks (1,024 + 4,096 + 180 ZMWs) split into cost-balanced
+    micro-batches over N >= 2 device contexts (CCSX_NGPU groups beyond the
+    visible GPUs are logical contexts on the same device):
+    byte-identical to one context, in input order (main.c:701-704,707-717),
+    and equal to the oracle."""
     fa = str(tmp_path / "in.fa")
     write(fa, 5300, 1000, 6)
     outs = []
-    for slots in ("1", "2"):
-        out = str(tmp_path / f"out{slots}.fa")
-        r = subprocess.run([BIN, "-A", "-j", "8", fa, out], env=dict(os.environ, CCSX_SLOTS=slots),
-                           capture_output=True, timeout=300)
-        assert r.returncode == 0, r.stderr.decode()
+    for ngpu, slots in (("1", "1"), ("3", "2"), ("2", "1")):
+        out = str(tmp_path / f"out{ngpu}_{slots}.fa")
+        _run(["-A", "-j", "8", fa, out], env=dict(CCSX_NGPU=ngpu, CCSX_SLOTS=slots))
         outs.append(open(out, "rb").read())
     assert outs[0].count(b">") == 5300
-    assert outs[0] == outs[1]
+    assert outs[1] == outs[0] and outs[2] == outs[0]
+    assert outs[0] == _expected(fa, 0)
+
+
+def test_cli_bam_input(tmp_path):
+    """BAM is the reference's default input (main.c:754): a BGZF subread BAM
+    gives the same CCS as the same records as FASTA with -A, and the oracle's."""
+    bam, fa = str(tmp_path / "in.bam"), str(tmp_path / "in.fa")
+    write_bam(bam, records(40, 1500, 7, hole0=100))
+    write(fa, 40, 1500, 7, hole0=100)
+    ob, of = str(tmp_path / "b.fa"), str(tmp_path / "f.fa")
+    _run(["-j", "4", bam, ob])
+    _run(["-A", "-j", "4", fa, of])
+    got = open(ob, "rb").read()
+    assert got.count(b">") == 40
+    assert got == open(of, "rb").read()
+    assert got == _expected(bam, 0, is_bam=True)
+
+
+def test_cli_failed_zmw_is_skipped(tmp_path):
+    """A ZMW the device reports as failed is skipped with a message; every
+    other ZMW is still written, in input order, and the run exits 0."""
+    fa = str(tmp_path / "in.fa")
+    write(fa, 30, 1200, 6)
+    out = str(tmp_path / "out.fa")
+    r = _run(["-A", "-j", "4", fa, out], env=dict(CCSX_FAULT_HOLE="7", CCSX_NGPU="2", CCSX_SLOTS="1"))
+    assert b"synth/7: no CCS" in r.stderr
+    got = open(out, "rb").read()
+    assert got.count(b">") == 29
+    assert got == _expected(fa, 0, exclude={"7"})
+
+
+def test_cli_verbose_segments(tmp_path):
+    """-v dumps every oriented segment as main.c:477-479 does (strand= field)."""
+    fa = str(tmp_path / "in.fa")
+    write(fa, 2, 1200, 6)
+    r = _run(["-A", "-v", fa, str(tmp_path / "o.fa")])
+    err = r.stderr.decode()
+    assert err.count(" strand=") == 12
+    assert ">0_0/6 strand=0 len=" in err

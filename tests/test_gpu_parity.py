@@ -131,3 +131,36 @@ def test_reads_shorter_than_band(engine, L, passes, mode):
     end invalid, the free end inside the band)."""
     zs = [synth(4000 + h, L, passes) for h in range(16)]
     _check(engine, zs, mode)
+
+
+def _e_shapes():
+    """Config E (bench.py zmw_shape) holes: the largest drawn shapes."""
+    import bench
+    cfg = bench.CONFIGS["E"]
+    shapes = [(h, *bench.zmw_shape(cfg, h)) for h in range(6000)]
+    big = [s for s in shapes if s[1] >= 20000 and s[2] >= 10]
+    top = max(shapes, key=lambda s: s[1] * s[2])
+    return big[:3] + [top]
+
+
+def test_config_e_largest_shapes(engine):
+    """Config E's largest ZMWs (>= 20 kb inserts x >= 10 passes and the
+    largest L x passes of 6,000 drawn holes, ~300 kb of subreads) through
+    ccsx_gpu_run (tight caps, full-cap re-run) vs the oracle, in one batch
+    with small ZMWs so the LPT launch order is exercised."""
+    import bench
+    zs = []
+    for h, L, p in _e_shapes():
+        subs, _ = cx.synth_zmw(bench.SEED, h, L, p)
+        zs.append(cx.prepare(subs))
+    zs += [synth(7000 + h, 2000, 6) for h in range(4)]
+    assert max(int(z.lens.sum()) for z in zs) > 250_000
+    _check(engine, zs, cx.MODE_SHRED)
+
+
+def test_zmw_near_max_total_length(engine):
+    """A ZMW near ccsx's -M cap (500 kb, main.c:662-665): 25 kb x 17 passes,
+    ~440 kb of subreads, shredded mode."""
+    zs = [synth(7100, 25000, 17)]
+    assert 400_000 < int(zs[0].lens.sum()) < 500_000
+    _check(engine, zs, cx.MODE_SHRED)
