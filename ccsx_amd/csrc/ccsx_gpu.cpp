@@ -199,6 +199,22 @@ const char *ccsx_gpu_status_str(int32_t s)
     }
 }
 
+// LDS read buffer limits of the LDS kernel instance: reads up to 100 kb
+// (50 KiB of nibble pairs, 2 workgroups per CU) and 4,096 segments; beyond
+// them a slice runs the HBM-read instance
+constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
+
+// launch classes of ccsx_gpu_run's slices: LDS read buffer up to 32 kb (4+
+// workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never
+// mix classes, so one long read does not shrink the occupancy of a slice
+static int zmw_class(const ccsx_zmw_in &zi)
+{
+    uint32_t lmax = 0;
+    for (uint32_t k = 0; k < zi.nseg; ++k) lmax = std::max(lmax, zi.seg_len[k]);
+    if (lmax > kLdsReadMaxBases || zi.nseg > kLdsMaxSegs) return 2;
+    return lmax > 32768 ? 1 : 0;
+}
+
 static void zmw_extent(const ccsx_zmw_in &zi, uint64_t &S, uint64_t &hi, uint32_t &lmax)
 {
     S = 0, hi = 0, lmax = 0;
@@ -262,9 +278,16 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     c->seq_bytes = seq_b, c->ws_bytes = ws_b, c->out_bytes = out_b, c->msa_bytes = msa_b;
     c->nseg_total = nseg;
     // nibble-pair read buffer (ccsx_kernel.hip load_read); at least one band:
-    // every lane reads its window bytes even when the read is shorter
-    c->lds_read_words = (std::max<uint32_t>(lmax_all, ccsx::kW) + 7) / 8 + 2;
-    c->lds_nmax = std::max<uint32_t>(nmax, 1);
+    // every lane reads its window bytes even when the read is shorter.  A
+    // slice with a read or a cursor array beyond the LDS budget runs the
+    // HBM-read kernel instance (lds_read_words = 0)
+    if (lmax_all > kLdsReadMaxBases || nmax > kLdsMaxSegs) {
+        c->lds_read_words = 0;
+        c->lds_nmax = 0;
+    } else {
+        c->lds_read_words = (std::max<uint32_t>(lmax_all, ccsx::kW) + 7) / 8 + 2;
+        c->lds_nmax = std::max<uint32_t>(nmax, 1);
+    }
     size_t freeb = 0, totb = 0;
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
     const uint64_t need = seq_b + ws_b + out_b + msa_b + uint64_t(nseg) * 8 + nz * (sizeof(ccsx::ZmwDesc) + 32);
@@ -451,6 +474,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     c->run_arena.clear();
     std::vector<uint64_t> aoff(nz, 0);
+    std::vector<int> cls(nz, 0);
     std::string first_err;
     auto run_list = [&](const std::vector<uint32_t> &idx, bool full, std::vector<uint32_t> *retry) -> int {
         size_t b = 0;
@@ -459,7 +483,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             size_t e = b;
             while (e < idx.size()) {
                 const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows);
-                if (e > b && need + x > budget) break;
+                if (e > b && (need + x > budget || cls[idx[e]] != cls[idx[b]])) break;
                 need += x;
                 ++e;
             }
@@ -506,7 +530,8 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         return 0;
     };
     std::vector<uint32_t> all(nz), retry;
-    for (size_t i = 0; i < nz; ++i) all[i] = uint32_t(i);
+    for (size_t i = 0; i < nz; ++i) all[i] = uint32_t(i), cls[i] = zmw_class(z[i]);
+    std::stable_sort(all.begin(), all.end(), [&](uint32_t x, uint32_t y) { return cls[x] < cls[y]; });
     int r = run_list(all, false, &retry);
     if (!r && !retry.empty()) r = run_list(retry, true, nullptr);
     if (r) return r;

@@ -218,6 +218,13 @@ __device__ __forceinline__ T *P(const Z &z, uint64_t off)
     return reinterpret_cast<T *>(z.ws + off);
 }
 
+// an extension region (ccsx_layout.h zext), offsets computed where used
+template <class T>
+__device__ __forceinline__ T *PX(const Z &z, int which)
+{
+    return reinterpret_cast<T *>(z.ws + z.L.ext + zext_bytes(z.d, which));
+}
+
 // graph buffer b (0/1) of the double-buffered rebuild (SPEC.md §5)
 __device__ __forceinline__ uint8_t *G_nb(const Z &z, int b) { return P<uint8_t>(z, b ? z.L.nb1 : z.L.nb0); }
 __device__ __forceinline__ uint64_t *G_mem(const Z &z, int b) { return P<uint64_t>(z, b ? z.L.mem1 : z.L.mem0); }
@@ -315,7 +322,11 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
 // 32-row traceback block, so the traceback's window fill -- 32 lanes reading
 // the same column of 32 consecutive rows -- spreads over the LDS banks instead
 // of hitting one (a 256 B pitch is a multiple of the 32-bank width).
+#ifdef CCSX_NO_ROT
+__device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return 0u * r; }  // (diagnostic variant)
+#else
 __device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; }
+#endif
 
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
@@ -853,8 +864,9 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
     const int32_t *ring = z.lds + kLdsRing;
     if (info & kInfoFar) {
         int32_t o = off;
-        // band placement is wave 0's; the cell tags are predecessor slots (6 bits)
-        if (np > 63) z.status = kErrInDegree;
+        // band placement is wave 0's; the cell tags are predecessor slots
+        // (6 bits in the record; rows above 63 predecessors: dpB_row also
+        // stores the full slots)
         far_terms<true>(z, r, np, vOff, 0, 0, false, o, A);
         return;
     }
@@ -930,8 +942,13 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
     const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
-    uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 << 4) | (A.ds0 << 10);
-    uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 << 4) | (A.ds1 << 10);
+    uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
+    uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
+    if (__builtin_expect(np > 63u, 0)) {
+        // wide slot record of row r: u16 M / D slots per cell
+        reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
+            make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
+    }
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
     // H' at j = m - 1
     const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
@@ -1172,9 +1189,18 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
     const uint32_t lane = lane_id();
     const uint8_t *src = z.ws + z.L.codes + (size_t)bi * kTbRows * 256 + lane * 16u;
     int32_t *dst = z.lds + buf * kTbBufWords;
+#ifdef CCSX_TB_DMA_B32
+    // (diagnostic variant: 4 B per lane, one row per instruction)
+    const uint8_t *s4 = z.ws + z.L.codes + (size_t)bi * kTbRows * 256 + lane * 4u;
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(s4 + k * 256), dst + k * 64, 4, 0, 0);
+    (void)src;
+#else
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(src + k * 1024), dst + k * 256, 16, 0, 0);
+#endif
     const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + bi * kTbRows + lane;
     __builtin_amdgcn_global_load_lds(ms, z.lds + 2 * kTbBufWords + buf * 64, 4, 0, 0);
 }
@@ -1285,10 +1311,20 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         }
         --j;
     };
-    // to the predecessor given by the cell's tag (a slot on far rows)
-    auto to_pred = [&](uint32_t tag) {
-        if ((farm >> (r - base)) & 1u) r = uni(pred[uni(poff[r]) + tag]);
-        else r -= tag;
+    // to the predecessor given by the tag of cell (r, jc) (a slot on far
+    // rows; D: the D tag); far rows above 63 predecessors keep their slots in
+    // the wide records
+    auto to_pred = [&](uint32_t tag, int32_t jc, uint32_t isD) {
+        if ((farm >> (r - base)) & 1u) {
+            const uint32_t p0 = uni(poff[r]);
+            if (uni(poff[r + 1]) - p0 > 63u) {
+                const uint32_t t = (uint32_t)(jc - __builtin_amdgcn_readlane((int)voff, (int)(r - base)));
+                tag = uni((uint32_t)PX<const uint16_t>(z, kExtWtag)[(size_t)r * (kW * 2) + t * 2 + isD]);
+            }
+            r = uni(pred[p0 + tag]);
+        } else {
+            r -= tag;
+        }
     };
     uint32_t rec = cell();
     for (;;) {
@@ -1370,7 +1406,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 probed = true;
             }
             step_j();
-            to_pred((rec >> 4) & 63u);
+            to_pred((rec >> 4) & 63u, j + 1, 0u);  // the MPRED cell is (r, j + 1)
             rec = cell();
             if (probed) DP_STAMP(kPfTbProbe);
             else DP_STAMP(kPfTbStep);
@@ -1387,7 +1423,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             // state D: follow D tags while the cell's D extends its predecessor's D
             for (;;) {
                 const uint32_t ext = rec & 4u;
-                to_pred((rec >> 10) & 63u);
+                to_pred((rec >> 10) & 63u, j, 1u);
                 rec = cell();
                 if (!ext || ++guard > glim) break;
             }
@@ -1469,7 +1505,14 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
 // LDS (idle during merge): the column walks, the count atomics, the prefix
 // scan and every shift lookup are then LDS accesses instead of dependent HBM
 // round trips.  Larger graphs (-P) take the same steps through HBM.
-__device__ __forceinline__ bool merge_in_lds(uint32_t R) { return (R + 1) * 5u + 64u <= (uint32_t)(kRingA * kRowW * 4); }
+__device__ __forceinline__ bool merge_in_lds(uint32_t R)
+{
+#ifdef CCSX_NO_LM
+    return false && R;  // (diagnostic variant: merge through HBM only)
+#else
+    return (R + 1) * 5u + 64u <= (uint32_t)(kRingA * kRowW * 4);
+#endif
+}
 
 template <bool LM>
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid)
@@ -1992,10 +2035,12 @@ __device__ __forceinline__ void write_msa(Z &z, uint32_t ncols, uint32_t n, uint
 #ifndef CCSX_WAVES_PER_EU
 #define CCSX_WAVES_PER_EU 4
 #endif
-__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(CCSX_WAVES_PER_EU)))
-ccsx_zmw_kernel(KArgs a)
+// RD_HBM: the instance for ZMWs whose reads do not fit the LDS read buffer
+// (or whose cursors do not): the read (nibble pairs) and the shredding cursors
+// live in the workspace; every other access is the same code.
+template <bool RD_HBM>
+__device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
 {
-    extern __shared__ int32_t smem[];
     if (blockIdx.x >= a.nzmw) return;
     // longest-processing-time-first: the host orders the batch by cost so the
     // largest ZMWs start first and the tail of the launch is short ones
@@ -2007,9 +2052,15 @@ ccsx_zmw_kernel(KArgs a)
     z.ws = a.ws + z.d.ws_off;
     z.seq = a.seq + z.d.seq_off;
     z.lds = smem;
-    z.rd = reinterpret_cast<uint8_t *>(smem + kLdsFixed);
-    z.pos = reinterpret_cast<uint32_t *>(smem + kLdsFixed) + a.lds_read_words;
-    z.rdcap = (a.lds_read_words - 2) * 8;
+    if (RD_HBM) {
+        z.rd = PX<uint8_t>(z, kExtRdbuf);
+        z.pos = PX<uint32_t>(z, kExtPos);
+        z.rdcap = z.d.lcap;
+    } else {
+        z.rd = reinterpret_cast<uint8_t *>(smem + kLdsFixed);
+        z.pos = reinterpret_cast<uint32_t *>(smem + kLdsFixed) + a.lds_read_words;
+        z.rdcap = (a.lds_read_words - 2) * 8;
+    }
     z.status = kOk;
     z.cells = 0;
 #pragma unroll
@@ -2051,7 +2102,7 @@ ccsx_zmw_kernel(KArgs a)
                 if (lane == 0) a.ncols[zi] = ncols;
             }
         }
-    } else if (n > a.lds_nmax) {
+    } else if (!RD_HBM && n > a.lds_nmax) {
         z.status = kErrReadLen;
     } else {
         // ccs_for2 (main.c:541-641)
@@ -2103,15 +2154,34 @@ ccsx_zmw_kernel(KArgs a)
     }
 }
 
+__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(CCSX_WAVES_PER_EU)))
+ccsx_zmw_kernel(KArgs a)
+{
+    extern __shared__ int32_t smem[];
+    zmw_body<false>(a, smem);
+}
+
+__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(CCSX_WAVES_PER_EU)))
+ccsx_zmw_kernel_hbm(KArgs a)
+{
+    extern __shared__ int32_t smem[];
+    zmw_body<true>(a, smem);
+}
+
 }  // namespace ccsx
 
+// lds_read_words == 0 selects the HBM-read instance (ccsx_gpu.cpp decides)
 extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s)
 {
+    const void *f = a->lds_read_words ? reinterpret_cast<const void *>(&ccsx::ccsx_zmw_kernel)
+                                      : reinterpret_cast<const void *>(&ccsx::ccsx_zmw_kernel_hbm);
     if (lds_bytes > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&ccsx::ccsx_zmw_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(ccsx::kBlockThreads), lds_bytes, s, *a);
+    if (a->lds_read_words)
+        hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(ccsx::kBlockThreads), lds_bytes, s, *a);
+    else
+        hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel_hbm, dim3(a->nzmw), dim3(ccsx::kBlockThreads), lds_bytes, s, *a);
     return hipGetLastError();
 }

@@ -34,7 +34,7 @@ enum Status : int32_t {
     kErrEdges = 2,     // edges exceed ecap
     kErrMulti = 3,     // (unused: kept so status values stay stable)
     kErrSpill = 4,     // spilled DP rows exceed scap
-    kErrInDegree = 5,  // node in-degree > 255
+    kErrInDegree = 5,  // (unused since wide slot records: kept so status values stay stable)
     kErrReadLen = 6,   // pushed read longer than the LDS read buffer
     kErrOut = 7,       // CCS longer than the output slab
     kErrTrace = 8,     // traceback did not terminate (internal error)
@@ -50,6 +50,7 @@ struct ZmwDesc {
     uint32_t seg0;      // index of the first segment in the segment arrays
     uint32_t n;         // number of segments (pushed reads)
     uint32_t rcap, ecap, lcap, scap, nw;
+    uint32_t wcap;      // rows of wide slot records (rcap if n > 64, else 0)
     uint32_t outcap;    // output slab capacity (bytes)
     uint32_t msacap;    // MSA slab capacity (bytes)
 };
@@ -59,10 +60,37 @@ struct ZLayout {
     uint64_t rmeta, spf, sslot, codes, spill, rrec, rp3;
     uint64_t ev, tgt, ipt, iinf, ifix, cnt, fixf, addp, cntn;
     uint64_t colof, cons, cmask, colrow, rdoff, rdlen, rfirst, rlast, rfc, rlc;
+    uint64_t ext;  // rarely used regions (zext): kept as one offset to spare registers
     uint64_t total;
 };
 
 CCSX_HD inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+// The extension regions, in order (offsets relative to ZLayout::ext):
+//  * ZMWs of more than 64 segments (whose far rows can have more than 63
+//    predecessors, more than a 6-bit slot tag holds): a wide slot record per
+//    row (per cell the M and D predecessor slots, u16 each: 512 B per row),
+//    written for rows above 63 predecessors only;
+//  * the HBM-read kernel instance (reads beyond the LDS read buffer): the read
+//    as nibble pairs and the shredding cursors.
+enum ZExt { kExtWtag = 0, kExtRdbuf, kExtPos, kExtEnd };
+
+CCSX_HD inline uint64_t zext_size(const ZmwDesc &d, int which)
+{
+    switch (which) {
+    case kExtWtag: return uint64_t(d.wcap) * kW * 4;
+    case kExtRdbuf: return uint64_t((d.lcap + 7) / 8 + 2) * 4;
+    default: return uint64_t(d.n) * 4;
+    }
+}
+
+// offset of extension region `which` from ZLayout::ext (= bytes of the ones before it)
+CCSX_HD inline uint64_t zext_bytes(const ZmwDesc &d, int which)
+{
+    uint64_t o = 0;
+    for (int i = 0; i < which; ++i) o = align256(o + zext_size(d, i));
+    return o;
+}
 
 CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 {
@@ -106,6 +134,7 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
     L.rlast = take(uint64_t(d.n) * 4);
     L.rfc = take(uint64_t(d.n) * 4);
     L.rlc = take(uint64_t(d.n) * 4);
+    L.ext = take(zext_bytes(d, kExtEnd));
     L.total = o;
 }
 
@@ -134,6 +163,9 @@ CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, boo
     }
     d.lcap = lmax + 16;
     d.nw = (n + 63) / 64 ? (n + 63) / 64 : 1;
+    // in-degree <= reads pushed before (one in-edge per target per read), so
+    // only ZMWs of >= 65 segments can have rows above 63 predecessors
+    d.wcap = n > 64 ? d.rcap : 0;
     d.outcap = uint32_t(S + 16);
 }
 
@@ -152,7 +184,7 @@ struct KArgs {
     unsigned long long *cells;
     int32_t mode;
     uint32_t nzmw;
-    uint32_t lds_read_words;
+    uint32_t lds_read_words;    // 0: the HBM-read kernel instance (read and cursors in the workspace)
     uint32_t lds_nmax;
     unsigned long long *prof;  // optional: kProfSlots shader-clock counters per ZMW (diagnostics)
 };

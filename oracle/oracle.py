@@ -39,6 +39,7 @@ def lib() -> C.CDLL:
         L.opoa_cells.restype = C.c_uint64
         L.opoa_nrows.argtypes = [C.c_void_p]
         L.opoa_nrows.restype = C.c_uint32
+        L.opoa_graph_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.ocsx_zmw.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                C.c_uint32, C.c_char_p]
         L.ocsx_zmw.restype = C.c_size_t
@@ -98,6 +99,12 @@ class Poa:
 
     def nrows(self) -> int:
         return int(self._L.opoa_nrows(self._g))
+
+    def max_indegree(self) -> int:
+        """Largest predecessor count of the current graph (after poa())."""
+        h = (C.c_uint64 * 8)()
+        self._L.opoa_graph_stats(self._g, h)
+        return int(h[2])
 
 
 def batch(zmws, mode: int = 0, nthreads: int = 1):

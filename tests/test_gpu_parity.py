@@ -8,7 +8,7 @@ import pytest
 
 import ccsx_amd as cx
 from oracle.oracle import Poa, batch
-from tests.zmw_cases import edge_cases, synth
+from tests.zmw_cases import edge_cases, high_indegree, raw, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -164,3 +164,39 @@ def test_zmw_near_max_total_length(engine):
     zs = [synth(7100, 25000, 17)]
     assert 400_000 < int(zs[0].lens.sum()) < 500_000
     _check(engine, zs, cx.MODE_SHRED)
+
+
+@pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
+def test_indegree_above_63(engine, mode):
+    """A far row with 74 predecessors: its cell tags do not fit the 6-bit slot
+    field, the helpers store the full slots in the wide records and the
+    traceback follows them (round 1 failed the ZMW with status 5)."""
+    from oracle.oracle import Poa
+    reads = high_indegree()
+    g = Poa()
+    g.poa(reads)
+    assert g.max_indegree() > 63
+    zs = [raw(reads), raw(high_indegree(8)), synth(7200, 1500, 6)]
+    _check(engine, zs, mode)
+
+
+@pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
+def test_read_beyond_lds_buffer(engine, mode):
+    """Segments of 110 kb (more than the LDS read buffer's 100 kb): the slice
+    runs the HBM-read kernel instance, in the same call as ordinary ZMWs."""
+    zs = [synth(7300, 110_000, 5), synth(7301, 3000, 6), synth(7302, 40_000, 5)]
+    _check(engine, zs, mode)
+
+
+def test_more_segments_than_lds_cursors(engine):
+    """4,200 segments of 60 bases (more than the 4,096 LDS shredding cursors):
+    the HBM-read instance keeps the cursors in the workspace."""
+    import random
+    rnd = random.Random(11)
+    ins = bytes(rnd.choice(b"ACGT") for _ in range(60))
+    segs = []
+    for _ in range(4200):
+        s = bytearray(ins)
+        s[rnd.randrange(60)] = rnd.choice(b"ACGT")
+        segs.append(bytes(s))
+    _check(engine, [raw(segs), synth(7400, 2000, 6)], cx.MODE_SHRED)

@@ -59,3 +59,16 @@ def edge_cases() -> dict[str, cx.Prepared]:
     cases["many_passes_short"] = raw([mutate(rng, ins[:1200]) for _ in range(40)])
     cases["over_64_reads"] = raw([mutate(rng, ins[:700]) for _ in range(70)])
     return cases
+
+
+def high_indegree(seed: int = 7):
+    """91 reads P + M[:k] + S (k = 100 .. 10): each deletes a different suffix
+    of M, so S's first node gets one in-edge per read -- a far row with more
+    than 63 predecessors (more than a 6-bit slot tag holds)."""
+    import random
+    rnd = random.Random(seed)
+
+    def rb(n):
+        return bytes(rnd.choice(b"ACGT") for _ in range(n))
+    P, M, S = rb(300), rb(100), rb(300)
+    return [P + M[:k] + S for k in range(100, 9, -1)]
