@@ -76,6 +76,7 @@ def build_product(verbose: bool = False) -> str:
         os.path.join(CSRC, "host", "pairwise.cpp"),
         os.path.join(CSRC, "host", "seqio.cpp"),
         os.path.join(CSRC, "host", "dispatch.cpp"),
+        os.path.join(CSRC, "host", "ingest.cpp"),
     ]
     common = ["-O3", "-std=c++17", "-fPIC", "-I" + INC, "-I" + CSRC, "-I" + os.path.join(CSRC, "host")]
     # the kernel's per-ZMW chains are latency-bound: the ILP-maximising machine

@@ -36,11 +36,12 @@
 
 #include "ccsx_gpu.h"
 #include "ccsx_host.h"
-#include "ccsx_seqio.h"
+#include "ingest.h"
 
 namespace {
 
 struct Zmw {
+    ccsx_ingest::ZmwRef ref;  // the subreads as spans of the input blocks (until assembled)
     std::string movie, hole, seqs;
     std::vector<uint32_t> lens;
     std::vector<uint32_t> seg_off, seg_len;
@@ -92,8 +93,10 @@ int usage()
     return 1;
 }
 
-// ccs_prepare + strand flip for every ZMW of the chunk on nthreads threads
-// (the CPU half of step 1, main.c:520-536, with its -v output)
+// Per ZMW of the chunk, on nthreads threads: the bases assembled from the
+// input blocks (the copy step 0 of the reference makes, main.c:674-685), then
+// ccs_prepare + strand flip (the CPU half of step 1, main.c:520-536, with its
+// -v output)
 void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
 {
     std::atomic<size_t> next(0);
@@ -101,6 +104,19 @@ void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
         std::string msg;
         for (size_t i; (i = next.fetch_add(1)) < zs.size();) {
             Zmw &z = zs[i];
+            z.movie = std::move(z.ref.movie);
+            z.hole = std::move(z.ref.hole);
+            z.seqs.resize(z.ref.total());
+            z.lens.resize(z.ref.recs.size());
+            size_t o = 0;
+            for (size_t k = 0; k < z.ref.recs.size(); ++k) {
+                const ccsx_ingest::Rec &r = z.ref.recs[k];
+                ccsx_ingest::write_bases(r, &z.seqs[o]);
+                z.lens[k] = r.len;
+                o += r.len;
+            }
+            ccsx_ingest::ZmwRef().recs.swap(z.ref.recs);
+            std::vector<std::shared_ptr<ccsx_ingest::Block>>().swap(z.ref.keep);
             const uint32_t n = (uint32_t)z.lens.size();
             z.seg_off.resize(n);
             z.seg_len.resize(n);
@@ -282,7 +298,10 @@ int main(int argc, char **argv)
     } else {
         return usage();
     }
-    ccsx_reader *rd = ccsx_reader_open(in_path, isbam);
+    if (nthreads < 1) nthreads = 1;
+    // step 0's input: blocks decompressed ahead on a producer thread (BGZF
+    // members inflated on the -j threads), records parsed as spans
+    auto rd = ccsx_ingest::ZmwSource::open(in_path, isbam != 0, nthreads);
     if (!rd) {
         fprintf(stderr, "Error: Failed to open infile!\n");
         return 1;
@@ -312,7 +331,6 @@ int main(int argc, char **argv)
         ccsx_gpu_set_mem_share(ctx[i], (uint32_t)per_dev[dev]);
         ccsx_gpu_set_prealloc(ctx[i], 1);
     }
-    if (nthreads < 1) nthreads = 1;
 
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     const auto tstart = std::chrono::steady_clock::now();
@@ -402,20 +420,15 @@ int main(int argc, char **argv)
         ch->id = id;
         std::vector<Zmw> &zs = ch->zs;
         const double t0 = now_ms();
-        const char *movie, *hole, *seqs;
-        const uint32_t *lens;
+        ccsx_ingest::ZmwRef zr;
         int l;
-        while ((l = ccsx_reader_next(rd, &movie, &hole, &seqs, &lens)) >= 0) {
+        while ((l = rd->next(zr)) >= 0) {
             if (l < min_fulllen_count + 2) continue;
-            size_t total = 0;
-            for (int i = 0; i < l; ++i) total += lens[i];
-            if (total > (size_t)max_subread_len || total < (size_t)min_subread_len) continue;
-            if (have_holes && hole_set.count(hole)) continue;
+            const uint64_t total = zr.total();
+            if (total > (uint64_t)max_subread_len || total < (uint64_t)min_subread_len) continue;
+            if (have_holes && hole_set.count(zr.hole)) continue;
             zs.emplace_back();
-            Zmw &z = zs.back();
-            z.movie = movie, z.hole = hole;
-            z.seqs.assign(seqs, total);
-            z.lens.assign(lens, lens + l);
+            zs.back().ref = std::move(zr);
             if (zs.size() >= chunk_size) {
                 chunk_size = std::min(chunk_size * 4, chunk_max);
                 break;
@@ -451,7 +464,7 @@ int main(int argc, char **argv)
     if (fatal) ring.stop();
     writer.join();
     for (auto *x : ctx) ccsx_gpu_close(x);
-    ccsx_reader_close(rd);
+    rd.reset();
     if (fp_out != stdout) fclose(fp_out);
     else fflush(stdout);
     if (nfail) fprintf(stderr, "[ccsx] %zu ZMWs had no CCS (device status, see above)\n", nfail);

@@ -39,6 +39,16 @@ def test_ingest_matches_reference(name):
     assert _product_calls(name, e["is_bam"]) == e["calls"]
 
 
+@pytest.mark.parametrize("block", [1, 7, 64, 4096])
+def test_ingest_across_block_boundaries(monkeypatch, block):
+    """The block-based parser (host/ingest.cpp) with blocks of a few bytes, so
+    every record, name, line ending and BAM record crosses blocks (the tail is
+    carried into the next block's headroom or, when larger, copied)."""
+    monkeypatch.setenv("CCSX_INGEST_BLOCK", str(block))
+    for name, e in sorted(EXPECTED.items()):
+        assert _product_calls(name, e["is_bam"]) == e["calls"], name
+
+
 def test_fixtures_cover_quirks():
     rets = {k: [c["ret"] for c in v["calls"]] for k, v in EXPECTED.items()}
     assert rets["invalid_name.fa"].count(-1) >= 2          # resumed after an invalid name

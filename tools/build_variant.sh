@@ -9,5 +9,5 @@ C=$ROOT/ccsx_amd/csrc
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include -I$C -I$C/host -mllvm -amdgpu-sched-strategy=max-ilp "$@" \
   -c $C/ccsx_kernel.hip -o $OBJ/ccsx_kernel_$TAG.hip.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/ccsx_amd/libccsx_amd_$TAG.so $OBJ/ccsx_kernel_$TAG.hip.o \
-  $OBJ/ccsx_gpu.cpp.o $OBJ/bspoa_gpu.cpp.o $OBJ/prepare.cpp.o $OBJ/pairwise.cpp.o $OBJ/seqio.cpp.o $OBJ/dispatch.cpp.o -lz -lpthread
+  $OBJ/ccsx_gpu.cpp.o $OBJ/bspoa_gpu.cpp.o $OBJ/prepare.cpp.o $OBJ/pairwise.cpp.o $OBJ/seqio.cpp.o $OBJ/dispatch.cpp.o $OBJ/ingest.cpp.o -lz -lpthread
 echo $ROOT/ccsx_amd/libccsx_amd_$TAG.so

@@ -42,8 +42,32 @@ def fastq(recs):
     return "".join(f"@{n}\n{s}\n+\n{'I' * len(s)}\n" for n, s in recs).encode()
 
 
+def bgzf(raw, block=20000):
+    """BGZF (SAM spec 4.1): deflate members of `block` bytes with the BC extra
+    field, then the empty end-of-file member; records span members."""
+    out = bytearray()
+    for i in range(0, len(raw) + 1, block):
+        d = raw[i:i + block]
+        if not d and i:
+            break
+        co = zlib.compressobj(6, zlib.DEFLATED, -15)
+        cd = co.compress(d) + co.flush()
+        out += struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, 18 + len(cd) + 8 - 1)
+        out += cd + struct.pack("<II", zlib.crc32(d) & 0xFFFFFFFF, len(d))
+    co = zlib.compressobj(6, zlib.DEFLATED, -15)
+    cd = co.compress(b"") + co.flush()
+    out += struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, 18 + len(cd) + 8 - 1)
+    out += cd + struct.pack("<II", 0, 0)
+    return bytes(out)
+
+
 def bam(recs):
     """Unaligned BAM (gzip-compressed; bamlite reads it through gzread)."""
+    return gzip.compress(bam_raw(recs), mtime=0)
+
+
+def bam_raw(recs):
+    """The uncompressed BAM stream of (name, seq) records."""
     text = b"@HD\tVN:1.5\tSO:unknown\n"
     body = b"BAM\x01" + struct.pack("<i", len(text)) + text + struct.pack("<i", 0)
     for name, seq in recs:
@@ -55,7 +79,7 @@ def bam(recs):
         core = struct.pack("<iiIIiiii", -1, -1, (4680 << 16) | (255 << 8) | len(rn), (4 << 16) | 0, l, -1, -1, 0)
         rec = core + rn + packed + qual
         body += struct.pack("<i", len(rec)) + rec
-    return gzip.compress(body)
+    return body
 
 
 def zmw(movie, hole, n, L, salt=0):
@@ -76,7 +100,7 @@ def cases():
     c["basic.fa"] = (0, fasta(base))
     c["multiline.fa"] = (0, fasta(base, width=17))
     c["basic.fq"] = (0, fastq(base))
-    c["basic.fa.gz"] = (0, gzip.compress(fasta(base)))
+    c["basic.fa.gz"] = (0, gzip.compress(fasta(base), mtime=0))
     iupac = [(n, s[:10] + "acgtNnRYKMSWBDHVU" + s[10:]) for n, s in zmw("mv", 3, 3, 30)]
     c["iupac_lower.fa"] = (0, fasta(iupac))
     # an invalid name in the middle of a ZMW (the reference keeps only the
@@ -95,7 +119,25 @@ def cases():
     emp = zmw("mv", 11, 2, 20) + [("mv/11/999_999", "")] + zmw("mv", 11, 2, 20, salt=2)
     c["empty_record.fa"] = (0, fasta(emp)[:-1])
     c["empty_fields.fa"] = (0, fasta([("mv//1_2", "ACGT"), ("/mv/1/2", "ACGT")] + zmw("mv", 12, 3, 20)))
+    # line-ending and blank-line quirks of kseq.h:178-218: CRLF (one '\r'
+    # stripped per appended line), blank lines inside and between records,
+    # a tab-terminated name, a lone '\r' line
+    crlf = fasta(base[:6], width=13).replace(b"\n", b"\r\n")
+    c["crlf.fa"] = (0, crlf)
+    c["crlf.fq"] = (0, fastq(base[:6]).replace(b"\n", b"\r\n"))
+    blank = b"".join(b">%s\tx=1\n\n%s\n\n%s\n\n" % (n.encode(), s[:7].encode(), s[7:].encode())
+                     for n, s in zmw("mv", 13, 4, 30))
+    c["blank_lines.fa"] = (0, b"junk before the first header\n" + blank + b">mv/14/0_3\nAC\r\n\r\nGT\n>mv/14/3_6\nACG\n")
+    # FASTQ quirks: quality lines starting with '@' / '>' and wrapped over
+    # several lines; a record with an empty sequence (kseq still reads one
+    # quality line: -2) after which reading goes on
+    fq = zmw("mvq", 15, 4, 30)
+    body = b"".join(b"@%s\n%s\n+\n%s\n%s\n" % (n.encode(), s.encode(), (b"@" + b">" * (len(s) // 2 - 1)),
+                                                  b"I" * (len(s) - len(s) // 2)) for n, s in fq)
+    c["fq_quirks.fq"] = (0, body + b"@mvq/16/0_0\n+\nIII\n" + fastq(zmw("mvq", 17, 3, 25)))
     c["basic.bam"] = (1, bam(base))
+    c["bgzf.bam"] = (1, bgzf(bam_raw(base + zmw("mvb", 21, 6, 3000))))
+    c["bgzf.fa.gz"] = (0, bgzf(fasta(base + zmw("mvb", 22, 5, 4000), width=61)))
     c["iupac.bam"] = (1, bam([(n, s[:5] + "NRYKM=" + s[5:]) for n, s in zmw("mvb", 3, 3, 31)]))
     c["invalid_name.bam"] = (1, bam(bad))
     return c
