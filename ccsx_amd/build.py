@@ -129,6 +129,16 @@ def build_oracle(verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
+    # the CPU-only ccsx of bench.py's cpu_baseline leg: the product's host
+    # C-ABI (ingest, ccs_prepare) around the oracle POA
+    cpu = os.path.join(ORACLE_DIR, "ccsx_cpu")
+    csrc = os.path.join(ORACLE_DIR, "ccsx_cpu.c")
+    if os.path.exists(LIB) and _stale(cpu, [csrc, LIB] + srcs + hdrs):
+        cmd = ["gcc", "-O2", "-std=gnu11", "-o", cpu, csrc] + srcs + ["-L" + HERE, "-lccsx_amd",
+                                                                       "-Wl,-rpath,$ORIGIN/../ccsx_amd", "-lpthread", "-lz"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
     return ORACLE_LIB
 
 

@@ -41,11 +41,13 @@ struct HostBuf {
         cap = 0;
         pinned = false;
     }
-    hipError_t reserve(size_t n)
+    // at least `floor` bytes (the CLI's contexts pin their staging once:
+    // re-pinning a grown arena costs ~0.25 s per GB)
+    hipError_t reserve(size_t n, size_t floor = 0)
     {
         if (n <= cap) return hipSuccess;
         release();
-        const size_t c = std::max<size_t>(n + n / 4, 4096);
+        const size_t c = std::max<size_t>(std::max<size_t>(n + n / 4, floor), 4096);
         hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p), c, hipHostMallocDefault);
         if (e == hipSuccess) {
             pinned = true;
@@ -113,6 +115,7 @@ struct ccsx_ctx {
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
     int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
+    bool shred_caps = false;           // tight caps sized for shredding windows (ccsx_gpu_run, shredded mode)
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
     bool prealloc = false;             // reserve the slice budget up front
     std::vector<uint8_t> run_arena;    // ccsx_gpu_run's gathered CCS strings
@@ -199,6 +202,10 @@ const char *ccsx_gpu_status_str(int32_t s)
     }
 }
 
+// pinned staging arenas of a preallocating context: big enough for a batch
+// of ~10k config-E ZMWs (1.3 GB of subreads) without re-pinning
+constexpr size_t kPinnedFloor = 2ull << 30;
+
 // LDS read buffer limits of the LDS kernel instance: reads up to 100 kb
 // (50 KiB of nibble pairs, 2 workgroups per CU) and 4,096 segments; beyond
 // them a slice runs the HBM-read instance
@@ -226,13 +233,13 @@ static void zmw_extent(const ccsx_zmw_in &zi, uint64_t &S, uint64_t &hi, uint32_
 }
 
 // device bytes one ZMW occupies when staged
-static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, uint32_t tight_rows)
+static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, uint32_t tight_rows, bool shred)
 {
     uint64_t S, hi;
     uint32_t lmax;
     zmw_extent(zi, S, hi, lmax);
     ccsx::ZmwDesc d{};
-    ccsx::zcaps(d, S, lmax, zi.nseg, full, tight_rows);
+    ccsx::zcaps(d, S, lmax, zi.nseg, full, tight_rows, shred);
     ccsx::ZLayout L;
     ccsx::zlayout(L, d);
     return ccsx::align256(L.total) + hi + d.outcap + uint64_t(zi.nseg) * 8 + sizeof(ccsx::ZmwDesc) + 32;
@@ -258,7 +265,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
             return -1;
         }
         ccsx::ZmwDesc &d = c->desc[i];
-        ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows);
+        ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows, c->shred_caps);
         d.seg0 = nseg;
         d.seq_off = seq_b;
         seq_b += hi;
@@ -289,6 +296,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
         c->lds_nmax = std::max<uint32_t>(nmax, 1);
     }
     size_t freeb = 0, totb = 0;
+    const auto ti = std::chrono::steady_clock::now();
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
     const uint64_t need = seq_b + ws_b + out_b + msa_b + uint64_t(nseg) * 8 + nz * (sizeof(ccsx::ZmwDesc) + 32);
     if (need + (1ull << 30) > freeb + c->d_ws.cap + c->d_seq.cap + c->d_out.cap + c->d_msa.cap) {
@@ -315,7 +323,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, c->d_cells.reserve(nz * 8));
     const auto tb = std::chrono::steady_clock::now();
     // host staging of the sequence arena and segment tables
-    HIPCHK(c, c->h_seq.reserve(seq_b));
+    HIPCHK(c, c->h_seq.reserve(seq_b, c->prealloc ? kPinnedFloor : 0));
     uint8_t *hseq = c->h_seq.p;
     std::vector<uint32_t> hoff(nseg), hlen(nseg);
     for (size_t i = 0; i < nz; ++i) {
@@ -344,8 +352,9 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, hipMemcpyAsync(c->d_order.p, order.data(), nz * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (timing)
-        fprintf(stderr, "[ccsx_gpu_stage] %zu ZMWs: reserve %.0f ms (ws cap %.1f GB), pack+copy %.1f MB %.0f ms\n", nz,
-                tms(tb - ta).count(), c->d_ws.cap / 1e9, seq_b / 1e6, tms(std::chrono::steady_clock::now() - tb).count());
+        fprintf(stderr, "[ccsx_gpu_stage] %zu ZMWs: meminfo %.0f ms, reserve %.0f ms (ws cap %.1f GB), pack+copy %.1f MB %.0f ms\n",
+                nz, tms(ta - ti).count(), tms(tb - ta).count(), c->d_ws.cap / 1e9, seq_b / 1e6,
+                tms(std::chrono::steady_clock::now() - tb).count());
     return 0;
 }
 
@@ -410,7 +419,7 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
     if (!c) return -1;
     HIPCHK(c, hipSetDevice(c->device));
     const size_t nz = c->nz;
-    HIPCHK(c, c->h_out.reserve(c->out_bytes));
+    HIPCHK(c, c->h_out.reserve(c->out_bytes, c->prealloc ? kPinnedFloor : 0));
     c->h_olen.resize(nz);
     c->h_status.resize(nz);
     c->h_cells.resize(nz);
@@ -453,6 +462,11 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         return -1;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    struct ShredCaps {  // the window-sized tight caps for this call only
+        ccsx_ctx *c;
+        ShredCaps(ccsx_ctx *x, bool on) : c(x) { c->shred_caps = on; }
+        ~ShredCaps() { c->shred_caps = false; }
+    } shred_caps(c, mode == CCSX_MODE_SHRED);
     size_t freeb = 0, totb = 0;
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
     // the workspace may grow into what is free plus what it already holds;
@@ -470,8 +484,14 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         const uint64_t part = totb / (2ull * c->mem_share);
         budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
     }
-    if (c->prealloc && c->d_ws.cap < budget) HIPCHK(c, c->d_ws.reserve(budget, true));
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
+    if (c->prealloc && c->d_ws.cap < budget) {
+        const auto t0 = std::chrono::steady_clock::now();
+        HIPCHK(c, c->d_ws.reserve(budget, true));
+        if (timing)
+            fprintf(stderr, "[ccsx_gpu_run] dev %d: workspace of %.1f GB reserved in %.0f ms\n", c->device, budget / 1e9,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
     c->run_arena.clear();
     std::vector<uint64_t> aoff(nz, 0);
     std::vector<int> cls(nz, 0);
@@ -482,7 +502,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             uint64_t need = 0;
             size_t e = b;
             while (e < idx.size()) {
-                const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows);
+                const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows, c->shred_caps);
                 if (e > b && (need + x > budget || cls[idx[e]] != cls[idx[b]])) break;
                 need += x;
                 ++e;
@@ -533,7 +553,10 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     for (size_t i = 0; i < nz; ++i) all[i] = uint32_t(i), cls[i] = zmw_class(z[i]);
     std::stable_sort(all.begin(), all.end(), [&](uint32_t x, uint32_t y) { return cls[x] < cls[y]; });
     int r = run_list(all, false, &retry);
-    if (!r && !retry.empty()) r = run_list(retry, true, nullptr);
+    if (!r && !retry.empty()) {
+        if (timing) fprintf(stderr, "[ccsx_gpu_run] dev %d: %zu ZMWs re-run with full caps\n", c->device, retry.size());
+        r = run_list(retry, true, nullptr);
+    }
     if (r) return r;
     if (c->fault >= 0 && (size_t)c->fault < nz) {
         out[c->fault].status = ccsx::kErrTrace;

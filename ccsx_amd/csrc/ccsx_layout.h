@@ -146,15 +146,20 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 // a fraction of the memory; every cap is checked on the device (kErrRows,
 // kErrEdges, kErrSpill) and ccsx_gpu_run re-runs a ZMW that hits
 // one with full caps.  tight_rows overrides the tight row cap (tests).
+// shred: the ZMW runs the shredded loop (main.c:541-641), whose POAs are of
+// 2 kb windows (+2 kb per missed breakpoint) rather than whole segments, so
+// the tight row cap follows the window, not the segment (rows ~ window x
+// (1 + ~0.07 reads): 3 x 8,000 + 4,096 covers windows up to ~8 kb).
 CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, bool full = true,
-                          uint32_t tight_rows = 0)
+                          uint32_t tight_rows = 0, bool shred = false)
 {
     d.n = n;
     d.rcap = uint32_t(S + 16);
     d.ecap = uint32_t(S + n + 16);
     d.scap = d.rcap / 4 + 64;
     if (!full) {
-        uint64_t r = tight_rows ? tight_rows : 3ull * lmax + 4096;
+        const uint64_t lw = shred && lmax > 8000u ? 8000u : lmax;
+        uint64_t r = tight_rows ? tight_rows : 3ull * lw + 4096;
         if (r < S) {
             d.rcap = uint32_t(r + 16);
             d.ecap = 2 * d.rcap;

@@ -59,3 +59,59 @@ uint32_t ccsx_partition(const uint64_t *cost, uint32_t n, uint32_t nparts, uint3
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Synthetic prepared batches for benchmarks (bench.py's end-to-end line):
+// ccsx_synth_zmw + ccsx_prepare_apply per ZMW on worker threads.
+#include <atomic>
+#include <memory>
+#include <string>
+#include <thread>
+
+#include "ccsx_gpu.h"
+
+struct ccsx_synth_batch {
+    std::vector<std::string> seqs;
+    std::vector<std::vector<uint32_t>> off, len;
+    std::vector<ccsx_zmw_in> in;
+};
+
+extern "C" {
+
+ccsx_synth_batch *ccsx_synth_batch_make(uint64_t seed, const uint64_t *holes, const uint32_t *L, const uint32_t *passes,
+                                        uint32_t n, int nthreads)
+{
+    auto *b = new ccsx_synth_batch();
+    b->seqs.resize(n);
+    b->off.resize(n);
+    b->len.resize(n);
+    b->in.resize(n);
+    std::atomic<uint32_t> nx(0);
+    auto work = [&]() {
+        std::vector<uint32_t> lens;
+        for (uint32_t i; (i = nx.fetch_add(1)) < n;) {
+            std::string &s = b->seqs[i];
+            s.resize((size_t)passes[i] * (2ull * L[i] + 16) + 16);
+            lens.resize(passes[i]);
+            const uint64_t tot = ccsx_synth_zmw(seed, holes[i], L[i], passes[i], &s[0], lens.data(), nullptr);
+            s.resize(tot);
+            b->off[i].resize(passes[i]);
+            b->len[i].resize(passes[i]);
+            const uint32_t ns = ccsx_prepare_apply(&s[0], lens.data(), passes[i], b->off[i].data(), b->len[i].data());
+            b->off[i].resize(ns);
+            b->len[i].resize(ns);
+            b->in[i] = ccsx_zmw_in{s.data(), b->off[i].data(), b->len[i].data(), ns};
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    return b;
+}
+
+const ccsx_zmw_in *ccsx_synth_batch_zmws(const ccsx_synth_batch *b) { return b->in.data(); }
+
+void ccsx_synth_batch_free(ccsx_synth_batch *b) { delete b; }
+
+}  // extern "C"

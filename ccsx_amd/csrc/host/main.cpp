@@ -10,9 +10,9 @@
 //     longest-first order (host/dispatch.cpp), queued behind the previous
 //     chunk's;
 //   * one worker thread per device context pulls batches from the queue and
-//     runs them through the batched C-ABI (include/ccsx_gpu.h); two contexts
-//     per GPU by default, so one stages and fetches while the other's kernel
-//     runs and the tail of one launch overlaps the next;
+//     runs them through the batched C-ABI (include/ccsx_gpu.h); one context
+//     per GPU by default (CCSX_SLOTS=2 runs two, whose launches overlap:
+//     measured no faster on config-E input);
 //   * a writer thread emits each chunk in input order once its last batch is
 //     back (main.c:707-717).
 // A ZMW the device cannot finish is reported on stderr and skipped; the other
@@ -83,7 +83,7 @@ int usage()
             "Environment:\n"
             "CCSX_NGPU      Number of GPU contexts groups [all visible GPUs]; more than the visible\n"
             "               GPUs places group g on GPU g %% visible (logical contexts)\n"
-            "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
+            "CCSX_SLOTS     Device contexts (worker threads) per group [1]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
             "\n"
             "Arguments:\n"
@@ -318,7 +318,7 @@ int main(int argc, char **argv)
     // CCSX_NGPU groups of CCSX_SLOTS contexts; group g on device g % ndev
     // (more groups than devices: logical contexts sharing a device, which is
     // how the multi-GPU split is exercised on a one-GPU box)
-    int ngroup = ndev, nslot = 2;
+    int ngroup = ndev, nslot = 1;
     if (const char *e = getenv("CCSX_NGPU")) ngroup = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("CCSX_SLOTS")) nslot = std::max(1, std::min(8, atoi(e)));
     const int nctx = ngroup * nslot;

@@ -27,7 +27,8 @@ EXPORTS = {
                    "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
-                    "ccsx_zmw_cost", "ccsx_partition"],
+                    "ccsx_zmw_cost", "ccsx_partition",
+                    "ccsx_synth_batch_make", "ccsx_synth_batch_zmws", "ccsx_synth_batch_free"],
     "ccsx_seqio.h": ["ccsx_reader_open", "ccsx_reader_next", "ccsx_reader_close"],
 }
 
@@ -88,6 +89,12 @@ def lib() -> C.CDLL:
         L.ccsx_partition.argtypes = [C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ccsx_partition.restype = C.c_uint32
+        L.ccsx_synth_batch_make.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                                            C.POINTER(C.c_uint32), C.c_uint32, C.c_int]
+        L.ccsx_synth_batch_make.restype = C.c_void_p
+        L.ccsx_synth_batch_zmws.argtypes = [C.c_void_p]
+        L.ccsx_synth_batch_zmws.restype = C.POINTER(ZmwIn)
+        L.ccsx_synth_batch_free.argtypes = [C.c_void_p]
         L.ccsx_reader_open.argtypes = [C.c_char_p, C.c_int]
         L.ccsx_reader_open.restype = C.c_void_p
         L.ccsx_reader_next.argtypes = [C.c_void_p] + [C.POINTER(C.c_char_p)] * 2 + [C.POINTER(C.c_void_p),
@@ -221,6 +228,27 @@ def read_zmws(path: str, is_bam: bool = False):
             yield movie, hole, subs
 
 
+class SynthBatch:
+    """ccsx_synth_batch_make: n synthetic ZMWs made and prepared on C threads."""
+
+    def __init__(self, seed: int, holes, Ls, passes, nthreads: int = 16):
+        n = len(holes)
+        h = np.ascontiguousarray(holes, dtype=np.uint64)
+        lv, pv = _u32(Ls), _u32(passes)
+        self._L = lib()
+        self.n = n
+        self._b = self._L.ccsx_synth_batch_make(seed, h.ctypes.data_as(C.POINTER(C.c_uint64)), _p32(lv), _p32(pv), n,
+                                                nthreads)
+        self.zmws = self._L.ccsx_synth_batch_zmws(self._b)
+        self.bases = sum(int(self.zmws[i].seg_len[k]) for i in range(n) for k in range(self.zmws[i].nseg))
+
+    def __del__(self):
+        try:
+            self._L.ccsx_synth_batch_free(self._b)
+        except Exception:
+            pass
+
+
 # ---------------------------------------------------------------- GPU engine
 class GpuError(RuntimeError):
     pass
@@ -297,6 +325,14 @@ class Engine:
             self._err("ccsx_gpu_run")
         return [(C.string_at(out[i].ccs, out[i].len) if out[i].len else b"", out[i].status, out[i].cells)
                 for i in range(len(zmws))]
+
+    def run_batch(self, batch: "SynthBatch", mode: int = MODE_SHRED):
+        """ccsx_gpu_run on a synthetic batch; returns [(status, cells)] (no CCS copy)."""
+        out = (ZmwOut * max(batch.n, 1))()
+        rc = self._L.ccsx_gpu_run(self._ctx, mode, batch.zmws, batch.n, out)
+        if rc != 0:
+            self._err("ccsx_gpu_run")
+        return [(out[i].status, out[i].cells, out[i].len) for i in range(batch.n)]
 
     def set_tight_rows(self, rows: int) -> None:
         """Test hook: override the tight row capacity (0 = default)."""

@@ -12,6 +12,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "ccsx_gpu.h" /* ccsx_zmw_in */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -59,6 +61,16 @@ uint32_t ccsx_partition(const uint64_t *cost, uint32_t n, uint32_t nparts, uint3
  * Returns the total number of bases written. */
 uint64_t ccsx_synth_zmw(uint64_t seed, uint64_t hole, uint32_t L, uint32_t passes,
                         char *out, uint32_t *lens, char *insert);
+
+/* Benchmarks: n synthetic ZMWs (ccsx_synth_zmw(seed, holes[i], L[i],
+ * passes[i]), then ccsx_prepare_apply) made on nthreads threads; the batch
+ * owns the data, ccsx_synth_batch_zmws gives the n push lists
+ * (ccsx_zmw_in, include/ccsx_gpu.h) ready for ccsx_gpu_run. */
+typedef struct ccsx_synth_batch ccsx_synth_batch;
+ccsx_synth_batch *ccsx_synth_batch_make(uint64_t seed, const uint64_t *holes, const uint32_t *L,
+                                        const uint32_t *passes, uint32_t n, int nthreads);
+const ccsx_zmw_in *ccsx_synth_batch_zmws(const ccsx_synth_batch *b);
+void ccsx_synth_batch_free(ccsx_synth_batch *b);
 
 #ifdef __cplusplus
 }

@@ -20,8 +20,8 @@ run_bench() {
   timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err && cat $OUT/bench.json
 }
 run_prof() {
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $R/bench.py --no-cpu-baseline > $OUT/kt_bench.json 2> $OUT/kt.err) &&
-  (cd /tmp && timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $OUT/pmc_lds -o p -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_lds.log 2>&1) &&
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $R/bench.py --no-cpu-baseline --e2e-zmws 0 > $OUT/kt_bench.json 2> $OUT/kt.err) &&
+  (cd /tmp && timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $OUT/pmc_lds -o p -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --e2e-zmws 0 > $OUT/pmc_lds.log 2>&1) &&
   echo "prof done"
 }
 case $WHAT in
