@@ -1421,7 +1421,13 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         }
         if (hc == HC_DEL) {
             // state D: follow D tags while the cell's D extends its predecessor's D
+#ifdef CCSX_DP_STAMPS
+            z.pf[kPfTbDruns] += 1;
+#endif
             for (;;) {
+#ifdef CCSX_DP_STAMPS
+                z.pf[kPfTbDsteps] += 1;
+#endif
                 const uint32_t ext = rec & 4u;
                 to_pred((rec >> 10) & 63u, j, 1u);
                 rec = cell();
@@ -1431,7 +1437,13 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             continue;
         }
         // state I: insertions along the row
+#ifdef CCSX_DP_STAMPS
+        z.pf[kPfTbIruns] += 1;
+#endif
         for (;;) {
+#ifdef CCSX_DP_STAMPS
+            z.pf[kPfTbIsteps] += 1;
+#endif
             emit((EV_INS << 30) | r);
             const uint32_t ext = rec & 8u;
             step_j();

@@ -213,6 +213,8 @@ enum ProfSlot { kPfTotal = 0, kPfLoad, kPfDp, kPfTrace, kPfMerge, kPfColumns, kP
                 // predecessor, two, other; spill rows; rows on the register
                 // path for predecessors r-1 / r-2): cycles, then counts
                 kPfCold0, kPfCold1, kPfCold2, kPfCold3, kPfCold4, kPfCold5, kPfCold6,
-                kPfColdN0, kPfColdN1, kPfColdN2, kPfColdN3, kPfColdN4, kPfColdN5, kPfColdN6, kProfSlots };
+                kPfColdN0, kPfColdN1, kPfColdN2, kPfColdN3, kPfColdN4, kPfColdN5, kPfColdN6,
+                // traceback (diagnostic build): insertion steps / runs, deletion steps / runs
+                kPfTbIsteps, kPfTbIruns, kPfTbDsteps, kPfTbDruns, kProfSlots };
 
 }  // namespace ccsx

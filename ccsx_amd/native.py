@@ -343,7 +343,8 @@ class Engine:
                   "a_busy", "a_wait", "b_busy", "b_wait", "tw_rows", "sw_rows", "spare2", "spare3",
                   "tb_probe", "tb_step", "tb_di", "tb_switch", "tb_nsw", "hw0", "hw1", "hw2", "start_rt", "end_rt", "a_head", "a_body", "a_tail", "a_fast",
                   "cold_far", "cold_chain", "cold_np1", "cold_np2", "cold_gen", "cold_spill", "cold_near",
-                  "n_far", "n_chain", "n_np1", "n_np2", "n_gen", "n_spill", "n_near")
+                  "n_far", "n_chain", "n_np1", "n_np2", "n_gen", "n_spill", "n_near",
+                  "tb_isteps", "tb_iruns", "tb_dsteps", "tb_druns")
 
     def set_profiling(self, on: bool = True) -> None:
         self._L.ccsx_gpu_set_profiling(self._ctx, 1 if on else 0)
