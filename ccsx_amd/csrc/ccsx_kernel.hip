@@ -297,8 +297,8 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
 //    insertion prefix-max and row-max scans, H; it writes each row's H and D
 //    to an LDS ring of kRingA rows, the exclusive prefix max (Pex) of the
 //    row's insertion scan and the row's band offset;
-//  * waves 1 and 2 (the helpers) follow one block of kBlkAB = 2 rows behind,
-//    one row each (wave 1 + h takes the rows of parity h): from the ring they
+//  * waves 1 and 2 (the helpers) follow one block of kBlkAB = 8 rows behind
+//    (wave 1 + h takes the rows of parity h): from the ring they
 //    recompute every cell's decision bits (SPEC.md §3.2-§3.4: MPRED / MSRC /
 //    DEL / INS, D-ext, I-ext), the predecessor slots of multi-predecessor
 //    rows and the free-end candidates, and store the row's records to HBM.
@@ -330,7 +330,10 @@ __device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; 
 
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
-constexpr int kBlkAB = 4;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2
+#ifndef CCSX_BLK
+#define CCSX_BLK 8
+#endif
+constexpr int kBlkAB = CCSX_BLK;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2, ...
 constexpr int kHelpers = 2;
 constexpr int kBlockThreads = 64 * (1 + kHelpers);
 static_assert(kBlkAB % kHelpers == 0, "each helper takes the same number of rows per block");

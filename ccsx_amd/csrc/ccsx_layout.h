@@ -20,7 +20,13 @@ namespace ccsx {
 constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
 constexpr int kRing = 16;      // DP rows kept in LDS per wave
 constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H and D, each [4 pad | 128 | 4 pad]
-constexpr int kRingA = 24;     // its ring rows: kRing predecessor rows + 2 blocks of the helpers' lag
+#ifndef CCSX_RINGA
+#define CCSX_RINGA 32
+#endif
+// its ring rows: kRing predecessor rows + 2 blocks of the helpers' lag (a
+// power of two: slot = row & 31; with 8-row blocks, measured 55.05 ms vs
+// 57.0 for 24 rows and 4-row blocks, tools/gpu_ab.sh r02o)
+constexpr int kRingA = CCSX_RINGA;
 constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 // fixed LDS words per workgroup: DP ring, helpers' diagnostic counters, band
