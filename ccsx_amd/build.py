@@ -28,6 +28,10 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 
 ARCH = os.environ.get("CCSX_OFFLOAD_ARCH", "gfx950")
+# the kernel configurations (ccsx_layout.h KernelCfg): latency (8-row DP
+# blocks, 32-row ring) and occupancy (4-row blocks, 24-row ring)
+KCFGS = [("lat", ["-DCCSX_KCFG=lat", "-DCCSX_LAUNCH=ccsx_launch_zmw_lat", "-DCCSX_RINGA=32", "-DCCSX_BLK=8"]),
+         ("occ", ["-DCCSX_KCFG=occ", "-DCCSX_LAUNCH=ccsx_launch_zmw_occ", "-DCCSX_RINGA=24", "-DCCSX_BLK=4"])]
 
 
 def _hipcc() -> str:
@@ -68,8 +72,9 @@ def build_product(verbose: bool = False) -> str:
     hipcc = _hipcc()
     os.makedirs(OBJ, exist_ok=True)
     hdrs = _headers()
+    khdrs = [os.path.join(CSRC, "ccsx_layout.h")]  # all the kernel includes
     srcs = [
-        os.path.join(CSRC, "ccsx_kernel.hip"),
+        os.path.join(CSRC, "ccsx_kernel.hip"),  # compiled once per kernel configuration (KCFGS)
         os.path.join(CSRC, "ccsx_gpu.cpp"),
         os.path.join(CSRC, "bspoa_gpu.cpp"),
         os.path.join(CSRC, "host", "prepare.cpp"),
@@ -84,13 +89,20 @@ def build_product(verbose: bool = False) -> str:
     kflags = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
     objs = []
     for s in srcs:
+        if s.endswith(".hip"):
+            for name, defs in KCFGS:
+                o = os.path.join(OBJ, f"ccsx_kernel_{name}.hip.o")
+                objs.append(o)
+                if _stale(o, [s] + khdrs):
+                    cmd = [hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + defs + ["-c", s, "-o", o]
+                    if verbose:
+                        print(" ".join(cmd))
+                    _run(cmd)
+            continue
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
         if _stale(o, [s] + hdrs):
-            if s.endswith(".hip"):
-                cmd = [hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + ["-c", s, "-o", o]
-            else:
-                cmd = [hipcc, "-x", "c++"] + common + ["-D__HIP_PLATFORM_AMD__", "-I" + _rocm_inc(), "-c", s, "-o", o]
+            cmd = [hipcc, "-x", "c++"] + common + ["-D__HIP_PLATFORM_AMD__", "-I" + _rocm_inc(), "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd))
             _run(cmd)
@@ -101,14 +113,18 @@ def build_product(verbose: bool = False) -> str:
         _run(cmd)
     # diagnostic variant with per-phase DP stamps (tools/phase_prof.py --diag)
     diag = os.path.join(HERE, "libccsx_amd_diag.so")
-    dobj = os.path.join(OBJ, "ccsx_kernel_diag.hip.o")
-    if _stale(dobj, [srcs[0]] + hdrs):
-        # the stamps' counters need registers: 2 waves per SIMD (occupancy is
-        # not what this build measures; per-ZMW cycle counts are)
-        _run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2"] + common
-             + kflags + ["-c", srcs[0], "-o", dobj])
-    if _stale(diag, objs[1:] + [dobj]):
-        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", diag, dobj] + objs[1:] + ["-lz", "-lpthread"])
+    dobjs = []
+    for name, defs in KCFGS:
+        dobj = os.path.join(OBJ, f"ccsx_kernel_{name}_diag.hip.o")
+        dobjs.append(dobj)
+        if _stale(dobj, [srcs[0]] + khdrs):
+            # the stamps' counters need registers: 2 waves per SIMD (occupancy
+            # is not what this build measures; per-ZMW cycle counts are)
+            _run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2"] + common
+                 + kflags + defs + ["-c", srcs[0], "-o", dobj])
+    host_objs = objs[len(KCFGS):]
+    if _stale(diag, host_objs + dobjs):
+        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", diag] + dobjs + host_objs + ["-lz", "-lpthread"])
     # the C host program
     main_src = os.path.join(CSRC, "host", "main.cpp")
     if os.path.exists(main_src) and _stale(BIN, [main_src, LIB] + hdrs):

@@ -18,7 +18,9 @@
 
 #include "ccsx_layout.h"
 
-extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+// the two kernel configurations (ccsx_layout.h KernelCfg), one object each
+extern "C" hipError_t ccsx_launch_zmw_lat(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+extern "C" hipError_t ccsx_launch_zmw_occ(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 
 namespace {
 
@@ -109,6 +111,10 @@ struct ccsx_ctx {
     // staged batch
     size_t nz = 0;
     uint32_t lds_read_words = 0, lds_nmax = 0;
+    int32_t cfg = ccsx::kCfgLatency;   // kernel configuration of the staged slice
+    int32_t cfg_force = -1;            // test hook: -1 = by slice size
+    uint32_t ncu = 256;                // compute units of the device
+    uint64_t reruns = 0;               // ZMWs ccsx_gpu_run re-ran with full caps
     uint64_t seq_bytes = 0, ws_bytes = 0, out_bytes = 0, msa_bytes = 0;
     uint32_t nseg_total = 0;
     std::vector<ccsx::ZmwDesc> desc;
@@ -162,6 +168,11 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0)
+            c->ncu = (uint32_t)n;
+    }
     if (e != hipSuccess) {
         fprintf(stderr, "[ccsx_gpu] cannot open device %d: %s\n", device, hipGetErrorString(e));
         delete c;
@@ -210,6 +221,8 @@ constexpr size_t kPinnedFloor = 2ull << 30;
 // (50 KiB of nibble pairs, 2 workgroups per CU) and 4,096 segments; beyond
 // them a slice runs the HBM-read instance
 constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
+// LDS read buffer of a tight-cap shredded slice (bases)
+constexpr uint32_t kShredReadCap = 8192;
 
 // launch classes of ccsx_gpu_run's slices: LDS read buffer up to 32 kb (4+
 // workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never
@@ -292,8 +305,24 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
         c->lds_read_words = 0;
         c->lds_nmax = 0;
     } else {
-        c->lds_read_words = (std::max<uint32_t>(lmax_all, ccsx::kW) + 7) / 8 + 2;
+        // shredded mode pushes windows of ~2-5 kb, not whole segments: with
+        // tight caps the buffer is capped at kShredReadCap bases (a longer
+        // window fails the ZMW with kErrReadLen and ccsx_gpu_run re-runs it
+        // uncapped), which keeps the LDS of config-E slices small enough for
+        // one more workgroup per CU
+        uint32_t lb = std::max<uint32_t>(lmax_all, ccsx::kW);
+        if (c->shred_caps && !full_caps) lb = std::min(lb, kShredReadCap);
+        c->lds_read_words = (lb + 7) / 8 + 2;
         c->lds_nmax = std::max<uint32_t>(nmax, 1);
+    }
+    // kernel configuration: the latency one if it keeps the whole slice
+    // resident (VGPRs: 16 waves per CU = 5 three-wave workgroups; LDS:
+    // 160 KiB), else the occupancy one (ccsx_layout.h KernelCfg)
+    {
+        const uint32_t lds_lat = uint32_t((ccsx::lds_fixed_words(ccsx::kCfgRingA[ccsx::kCfgLatency]) +
+                                           c->lds_read_words + c->lds_nmax) * 4);
+        const uint32_t wg = std::min<uint32_t>(5u, (160u * 1024u) / lds_lat);
+        c->cfg = c->cfg_force >= 0 ? c->cfg_force : (nz <= (size_t)c->ncu * wg ? ccsx::kCfgLatency : ccsx::kCfgOccupancy);
     }
     size_t freeb = 0, totb = 0;
     const auto ti = std::chrono::steady_clock::now();
@@ -390,13 +419,14 @@ int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
         HIPCHK(c, c->d_prof.reserve(c->nz * ccsx::kProfSlots * 8));
         a.prof = c->d_prof.as<unsigned long long>();
     }
-    const uint32_t lds = uint32_t((ccsx::kLdsFixedWords + c->lds_read_words + c->lds_nmax) * 4);
+    const uint32_t lds = uint32_t((ccsx::lds_fixed_words(ccsx::kCfgRingA[c->cfg]) + c->lds_read_words + c->lds_nmax) * 4);
     if (lds > 160 * 1024) {
         c->err = "reads too long for the LDS read buffer";
         return -1;
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, ccsx_launch_zmw(&a, lds, c->stream));
+    HIPCHK(c, c->cfg == ccsx::kCfgLatency ? ccsx_launch_zmw_lat(&a, lds, c->stream)
+                                           : ccsx_launch_zmw_occ(&a, lds, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     HIPCHK(c, hipEventSynchronize(c->ev1));
     float ms = 0.f;
@@ -447,9 +477,11 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
     return bad ? -2 : 0;
 }
 
+// statuses of a tight-cap slice that the full-cap (uncapped read buffer) re-run clears
 static bool is_cap_error(int32_t s)
 {
-    return s == ccsx::kErrRows || s == ccsx::kErrEdges || s == ccsx::kErrMulti || s == ccsx::kErrSpill;
+    return s == ccsx::kErrRows || s == ccsx::kErrEdges || s == ccsx::kErrMulti || s == ccsx::kErrSpill ||
+           s == ccsx::kErrReadLen;
 }
 
 // One chunk.  The chunk is cut into slices that fit the device's free memory
@@ -555,6 +587,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     int r = run_list(all, false, &retry);
     if (!r && !retry.empty()) {
         if (timing) fprintf(stderr, "[ccsx_gpu_run] dev %d: %zu ZMWs re-run with full caps\n", c->device, retry.size());
+        c->reruns += retry.size();
         r = run_list(retry, true, nullptr);
     }
     if (r) return r;
@@ -578,6 +611,17 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *c, uint32_t rows)
     c->tight_rows = rows;
     return 0;
 }
+
+int ccsx_gpu_set_kernel_cfg(ccsx_ctx *c, int cfg)
+{
+    if (!c || cfg < -1 || cfg > 1) return -1;
+    c->cfg_force = cfg;
+    return 0;
+}
+
+int ccsx_gpu_kernel_cfg(const ccsx_ctx *c) { return c ? c->cfg : -1; }
+
+int64_t ccsx_gpu_rerun_count(const ccsx_ctx *c) { return c ? (int64_t)c->reruns : -1; }
 
 int ccsx_gpu_set_fault(ccsx_ctx *c, int64_t zmw)
 {

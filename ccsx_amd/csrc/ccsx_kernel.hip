@@ -18,7 +18,18 @@
 
 #include "ccsx_layout.h"
 
+// One compilation per kernel configuration (ccsx_layout.h KernelCfg): the
+// build passes CCSX_RINGA / CCSX_BLK and names the configuration's namespace
+// and launcher, so the two objects link into one library side by side.
+#ifndef CCSX_KCFG
+#define CCSX_KCFG lat
+#endif
+#ifndef CCSX_LAUNCH
+#define CCSX_LAUNCH ccsx_launch_zmw_lat
+#endif
+
 namespace ccsx {
+namespace CCSX_KCFG {
 
 constexpr int kO = -3, kE = -2, kMs = 2, kXs = -6;  // main.c:842-847
 enum { HC_MPRED = 0, HC_MSRC = 1, HC_DEL = 2, HC_INS = 3 };
@@ -2203,20 +2214,22 @@ ccsx_zmw_kernel_hbm(KArgs a)
     zmw_body<true>(a, smem);
 }
 
+}  // namespace CCSX_KCFG
 }  // namespace ccsx
 
 // lds_read_words == 0 selects the HBM-read instance (ccsx_gpu.cpp decides)
-extern "C" hipError_t ccsx_launch_zmw(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s)
+extern "C" hipError_t CCSX_LAUNCH(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s)
 {
-    const void *f = a->lds_read_words ? reinterpret_cast<const void *>(&ccsx::ccsx_zmw_kernel)
-                                      : reinterpret_cast<const void *>(&ccsx::ccsx_zmw_kernel_hbm);
+    namespace K = ccsx::CCSX_KCFG;
+    const void *f = a->lds_read_words ? reinterpret_cast<const void *>(&K::ccsx_zmw_kernel)
+                                      : reinterpret_cast<const void *>(&K::ccsx_zmw_kernel_hbm);
     if (lds_bytes > 65536) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
         if (e != hipSuccess) return e;
     }
     if (a->lds_read_words)
-        hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel, dim3(a->nzmw), dim3(ccsx::kBlockThreads), lds_bytes, s, *a);
+        hipLaunchKernelGGL(K::ccsx_zmw_kernel, dim3(a->nzmw), dim3(K::kBlockThreads), lds_bytes, s, *a);
     else
-        hipLaunchKernelGGL(ccsx::ccsx_zmw_kernel_hbm, dim3(a->nzmw), dim3(ccsx::kBlockThreads), lds_bytes, s, *a);
+        hipLaunchKernelGGL(K::ccsx_zmw_kernel_hbm, dim3(a->nzmw), dim3(K::kBlockThreads), lds_bytes, s, *a);
     return hipGetLastError();
 }

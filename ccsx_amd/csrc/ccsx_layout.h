@@ -31,7 +31,19 @@ constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 // fixed LDS words per workgroup: DP ring, helpers' diagnostic counters, band
 // offsets, job; the read and the shredding cursors follow (ccsx_kernel.hip)
-constexpr int kLdsFixedWords = kRingA * kRowW + 32 + 64 + 16;
+// fixed LDS words of a kernel configuration with a ring of `ringa` rows
+CCSX_HD constexpr int lds_fixed_words(int ringa) { return ringa * kRowW + 32 + 64 + 16; }
+constexpr int kLdsFixedWords = lds_fixed_words(kRingA);
+
+// The two LDS kernel configurations (ccsx_kernel.hip is compiled once per
+// configuration, ccsx_gpu.cpp picks one per slice):
+//  * latency: 8-row lockstep blocks and a 32-row ring -- the shortest
+//    per-ZMW chain, 4 workgroups per CU (config B: 1,000 ZMWs in one wave of
+//    workgroups);
+//  * occupancy: 4-row blocks and a 24-row ring -- 5 workgroups per CU, for
+//    slices larger than the latency configuration keeps resident.
+enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1 };
+constexpr int kCfgRingA[2] = {32, 24};
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
 enum Status : int32_t {
@@ -41,7 +53,7 @@ enum Status : int32_t {
     kErrMulti = 3,     // (unused: kept so status values stay stable)
     kErrSpill = 4,     // spilled DP rows exceed scap
     kErrInDegree = 5,  // (unused since wide slot records: kept so status values stay stable)
-    kErrReadLen = 6,   // pushed read longer than the LDS read buffer
+    kErrReadLen = 6,   // pushed read longer than the LDS read buffer (re-run with an uncapped buffer)
     kErrOut = 7,       // CCS longer than the output slab
     kErrTrace = 8,     // traceback did not terminate (internal error)
 };

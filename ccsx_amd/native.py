@@ -24,7 +24,8 @@ EXPORTS = {
     "ccsx_gpu.h": ["ccsx_gpu_device_count", "ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
                    "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows",
-                   "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault"],
+                   "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault",
+                   "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
                     "ccsx_zmw_cost", "ccsx_partition",
@@ -72,6 +73,10 @@ def lib() -> C.CDLL:
         if hasattr(L, "ccsx_gpu_profile_zmw"):  # diagnostics; absent from older builds used in A/B runs
             L.ccsx_gpu_profile_zmw.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32]
         L.ccsx_gpu_set_tight_rows.argtypes = [C.c_void_p, C.c_uint32]
+        L.ccsx_gpu_set_kernel_cfg.argtypes = [C.c_void_p, C.c_int]
+        L.ccsx_gpu_kernel_cfg.argtypes = [C.c_void_p]
+        L.ccsx_gpu_rerun_count.argtypes = [C.c_void_p]
+        L.ccsx_gpu_rerun_count.restype = C.c_int64
         L.ccsx_revcomp.argtypes = [C.c_char_p, C.c_uint32]
         L.ccsx_prepare.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]
@@ -333,6 +338,18 @@ class Engine:
         if rc != 0:
             self._err("ccsx_gpu_run")
         return [(out[i].status, out[i].cells, out[i].len) for i in range(batch.n)]
+
+    def set_kernel_cfg(self, cfg: int) -> None:
+        """-1 = by slice size, 0 = latency (8-row blocks), 1 = occupancy (4-row blocks)."""
+        if self._L.ccsx_gpu_set_kernel_cfg(self._ctx, cfg) != 0:
+            self._err("ccsx_gpu_set_kernel_cfg")
+
+    def kernel_cfg(self) -> int:
+        return int(self._L.ccsx_gpu_kernel_cfg(self._ctx))
+
+    def rerun_count(self) -> int:
+        """ZMWs run() has re-run with full caps so far."""
+        return int(self._L.ccsx_gpu_rerun_count(self._ctx))
 
     def set_tight_rows(self, rows: int) -> None:
         """Test hook: override the tight row capacity (0 = default)."""

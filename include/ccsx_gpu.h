@@ -94,6 +94,15 @@ uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *ctx);
 int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
 /* Test hook: tight row capacity override (0 = default 3 x longest segment + 4096). */
 int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
+/* Kernel configuration of the next slices: -1 (default) = by slice size (the
+ * latency configuration -- 8-row DP blocks, 32-row LDS ring -- when it keeps
+ * the whole slice resident, else the occupancy one -- 4-row blocks, 24-row
+ * ring, one more workgroup per CU); 0 / 1 force one (tests, A/B).
+ * ccsx_gpu_kernel_cfg: the configuration of the last staged slice. */
+int ccsx_gpu_set_kernel_cfg(ccsx_ctx *ctx, int cfg);
+int ccsx_gpu_kernel_cfg(const ccsx_ctx *ctx);
+/* ZMWs ccsx_gpu_run has re-run with full caps on this context so far. */
+int64_t ccsx_gpu_rerun_count(const ccsx_ctx *ctx);
 /* Test hook: the next ccsx_gpu_run reports ZMW `zmw` (index into its batch)
  * as failed (status 8) after computing it, as a device failure would; the
  * run returns -2 and the other ZMWs are valid.  -1 = off. */

@@ -200,3 +200,29 @@ def test_more_segments_than_lds_cursors(engine):
         s[rnd.randrange(60)] = rnd.choice(b"ACGT")
         segs.append(bytes(s))
     _check(engine, [raw(segs), synth(7400, 2000, 6)], cx.MODE_SHRED)
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
+def test_both_kernel_configs(engine, cfg, mode):
+    """The latency (8-row DP blocks, 32-row ring) and occupancy (4-row blocks,
+    24-row ring) kernel objects, each forced, on a mixed batch: short reads,
+    a wide graph, ordinary ZMWs (the by-size choice picks only one of them
+    for small test batches)."""
+    zs = [synth(7400 + h, L, p) for h, (L, p) in enumerate([(2000, 8), (100, 12), (1500, 70), (4000, 6), (7000, 5)])]
+    engine.set_kernel_cfg(cfg)
+    try:
+        _check(engine, zs, mode)
+        assert engine.kernel_cfg() == cfg
+    finally:
+        engine.set_kernel_cfg(-1)
+
+
+def test_shred_window_beyond_read_cap(engine):
+    """Shredded ZMWs whose pushed windows exceed the 8,192-base read buffer of
+    a tight-cap slice (with two passes the whole 12 kb and 9 kb segments are
+    pushed, main.c:555-567): kErrReadLen, re-run uncapped, oracle parity."""
+    zs = [synth(7500, 12000, 2), synth(7501, 2000, 8), synth(7502, 9000, 2)]
+    before = engine.rerun_count()
+    _check(engine, zs, cx.MODE_SHRED)
+    assert engine.rerun_count() - before >= 2
