@@ -16,6 +16,7 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -68,6 +69,16 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError("build failed: " + " ".join(cmd))
 
 
+def _run_all(cmds: list[list[str]], verbose: bool = False) -> None:
+    if verbose:
+        for c in cmds:
+            print(" ".join(c))
+    jobs = int(os.environ.get("CCSX_BUILD_JOBS", "6"))
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(_run, c) for c in cmds]:
+            f.result()
+
+
 def build_product(verbose: bool = False) -> str:
     hipcc = _hipcc()
     os.makedirs(OBJ, exist_ok=True)
@@ -87,32 +98,22 @@ def build_product(verbose: bool = False) -> str:
     # the kernel's per-ZMW chains are latency-bound: the ILP-maximising machine
     # scheduler measured -0.8 % per launch on config B (tools/abn.sh)
     kflags = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-    objs = []
+    # every object is independent: compile them concurrently (the kernel
+    # objects take minutes each; host objects seconds)
+    objs, jobs = [], []
     for s in srcs:
         if s.endswith(".hip"):
             for name, defs in KCFGS:
                 o = os.path.join(OBJ, f"ccsx_kernel_{name}.hip.o")
                 objs.append(o)
                 if _stale(o, [s] + khdrs):
-                    cmd = [hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + defs + ["-c", s, "-o", o]
-                    if verbose:
-                        print(" ".join(cmd))
-                    _run(cmd)
+                    jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + defs + ["-c", s, "-o", o])
             continue
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
         if _stale(o, [s] + hdrs):
-            cmd = [hipcc, "-x", "c++"] + common + ["-D__HIP_PLATFORM_AMD__", "-I" + _rocm_inc(), "-c", s, "-o", o]
-            if verbose:
-                print(" ".join(cmd))
-            _run(cmd)
-    if _stale(LIB, objs):
-        cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lpthread"]
-        if verbose:
-            print(" ".join(cmd))
-        _run(cmd)
+            jobs.append([hipcc, "-x", "c++"] + common + ["-D__HIP_PLATFORM_AMD__", "-I" + _rocm_inc(), "-c", s, "-o", o])
     # diagnostic variant with per-phase DP stamps (tools/phase_prof.py --diag)
-    diag = os.path.join(HERE, "libccsx_amd_diag.so")
     dobjs = []
     for name, defs in KCFGS:
         dobj = os.path.join(OBJ, f"ccsx_kernel_{name}_diag.hip.o")
@@ -120,8 +121,15 @@ def build_product(verbose: bool = False) -> str:
         if _stale(dobj, [srcs[0]] + khdrs):
             # the stamps' counters need registers: 2 waves per SIMD (occupancy
             # is not what this build measures; per-ZMW cycle counts are)
-            _run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2"] + common
-                 + kflags + defs + ["-c", srcs[0], "-o", dobj])
+            jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2"]
+                        + common + kflags + defs + ["-c", srcs[0], "-o", dobj])
+    _run_all(jobs, verbose)
+    if _stale(LIB, objs):
+        cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lpthread"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+    diag = os.path.join(HERE, "libccsx_amd_diag.so")
     host_objs = objs[len(KCFGS):]
     if _stale(diag, host_objs + dobjs):
         _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", diag] + dobjs + host_objs + ["-lz", "-lpthread"])

@@ -6,6 +6,7 @@
 // This is the device boundary that replaces kt_for(ccs_for2/ccs_for) in step 1
 // of ccsx's pipeline (main.c:698-706).
 #include "ccsx_gpu.h"
+#include "ccsx_host.h"
 
 #include <chrono>
 #include <hip/hip_runtime.h>
@@ -371,13 +372,15 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, hipMemcpyAsync(c->d_slen.p, hlen.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_desc.p, c->desc.data(), nz * sizeof(ccsx::ZmwDesc), hipMemcpyHostToDevice,
                              c->stream));
-    // launch order: decreasing total bases (the POA work of a ZMW grows with
-    // it in both modes), ties in input order
+    // launch order: decreasing estimated POA work (ccsx_zmw_cost: S x (28 +
+    // n)), ties in input order -- longest-processing-time first, so a launch
+    // ends on its cheapest ZMWs.  (Round 1 ordered by rcap, which the tight
+    // shredded caps clamp to one value for every segment above 8 kb: config-E
+    // slices launched in input order.)
     std::vector<uint32_t> order(nz);
-    for (size_t i = 0; i < nz; ++i) order[i] = uint32_t(i);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-        return c->desc[x].rcap > c->desc[y].rcap;
-    });
+    std::vector<uint64_t> cost(nz);
+    for (size_t i = 0; i < nz; ++i) order[i] = uint32_t(i), cost[i] = ccsx_zmw_cost(z[i].seg_len, z[i].nseg);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
     HIPCHK(c, hipMemcpyAsync(c->d_order.p, order.data(), nz * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (timing)
@@ -581,9 +584,15 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         }
         return 0;
     };
+    // slices: by launch class, then most expensive first -- when a call needs
+    // several slices, the last one holds the cheapest ZMWs, whose launch (a
+    // few waves of workgroups) ends soonest
     std::vector<uint32_t> all(nz), retry;
-    for (size_t i = 0; i < nz; ++i) all[i] = uint32_t(i), cls[i] = zmw_class(z[i]);
-    std::stable_sort(all.begin(), all.end(), [&](uint32_t x, uint32_t y) { return cls[x] < cls[y]; });
+    std::vector<uint64_t> cost(nz);
+    for (size_t i = 0; i < nz; ++i)
+        all[i] = uint32_t(i), cls[i] = zmw_class(z[i]), cost[i] = ccsx_zmw_cost(z[i].seg_len, z[i].nseg);
+    std::stable_sort(all.begin(), all.end(),
+                     [&](uint32_t x, uint32_t y) { return cls[x] != cls[y] ? cls[x] < cls[y] : cost[x] > cost[y]; });
     int r = run_list(all, false, &retry);
     if (!r && !retry.empty()) {
         if (timing) fprintf(stderr, "[ccsx_gpu_run] dev %d: %zu ZMWs re-run with full caps\n", c->device, retry.size());

@@ -222,6 +222,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t 
     do {               \
     } while (0)
 #endif
+// traceback step counters (and block-switch cycles): the diagnostic build,
+// or a product build with -DCCSX_TB_COUNT (tools/phase_prof.py)
+#if defined(CCSX_DP_STAMPS) || defined(CCSX_TB_COUNT)
+#define CCSX_TB_COUNTING 1
+#endif
 
 template <class T>
 __device__ __forceinline__ T *P(const Z &z, uint64_t off)
@@ -1243,6 +1248,75 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
     __builtin_amdgcn_global_load_lds(ms, z.lds + 2 * kTbBufWords + buf * 64, 4, 0, 0);
 }
 
+// Plain MPRED steps k..3 of an aligned 4-column record window (traceback;
+// columns jw - 1 .. jw - 4 of the staged block's 32 rows, layout at vrot32):
+// per step, emit ALN | r at lane j & 63; leave with st = 1, unmoved, when the
+// cell's predecessor lies outside the block (tag >= r - base) or, on the
+// window's last column (j = 0 mod 4), when j completes a 64-base chunk; else
+// j -= 1, r -= tag and, below the last column, read the next record from the
+// window (lane (r - base) + 32 for columns 2 and 3, low / high half for even
+// / odd columns) and leave with st = 2 when it is not MPRED.  st = 0: moved
+// past the last column (the caller swaps in the next window).  Hand-written:
+// compiled, the multi-exit unrolled loop became a flag-driven state machine
+// of ~35 scalar instructions per step; here a step is 14.  (Measured: the
+// walk is latency-bound, ~150 cycles per step either way; this form is 0.3 %
+// faster per launch.  Handling D / I steps inside the window as well measured
+// no faster: tools/gpu_ab.sh r02u.)
+__device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t win, uint32_t &r, int32_t &j,
+                                            uint32_t &rec, uint32_t &vev, uint32_t &st)
+{
+    uint32_t t, li, m0v;
+    // the asm's scalar operands must live in SGPRs
+    r = uni(r), j = uni(j), rec = uni(rec), k = uni(k), base = uni(base);
+#define TBW_HEAD                                         \
+    "s_and_b32 %[m0], %[j], 63\n\t"                      \
+    "v_writelane_b32 %[vev], %[r], %[m0]\n\t"            \
+    "s_bfe_u32 %[t], %[rec], 0x60004\n\t"                \
+    "s_sub_u32 %[li], %[r], %[base]\n\t"                 \
+    "s_cmp_ge_u32 %[t], %[li]\n\t"                       \
+    "s_cbranch_scc1 .Ltbw_slow%=\n\t"
+#define TBW_MOVE                                         \
+    "s_sub_u32 %[j], %[j], 1\n\t"                        \
+    "s_sub_u32 %[r], %[r], %[t]\n\t"
+#define TBW_NEXT(LANEOR, HALF)                           \
+    "s_sub_u32 %[li], %[r], %[base]\n\t" LANEOR          \
+    "v_readlane_b32 %[rec], %[win], %[li]\n\t" HALF      \
+    "s_and_b32 %[t], %[rec], 3\n\t"                      \
+    "s_cbranch_scc1 .Ltbw_out%=\n\t"
+    asm volatile(
+        "s_cmp_eq_u32 %[k], 0\n\t"
+        "s_cbranch_scc1 .Ltbw_0%=\n\t"
+        "s_cmp_eq_u32 %[k], 1\n\t"
+        "s_cbranch_scc1 .Ltbw_1%=\n\t"
+        "s_cmp_eq_u32 %[k], 2\n\t"
+        "s_cbranch_scc1 .Ltbw_2%=\n\t"
+        "s_branch .Ltbw_3%=\n"
+        ".Ltbw_0%=:\n\t" TBW_HEAD TBW_MOVE TBW_NEXT("", "s_lshr_b32 %[rec], %[rec], 16\n\t")
+        ".Ltbw_1%=:\n\t" TBW_HEAD TBW_MOVE TBW_NEXT("s_or_b32 %[li], %[li], 32\n\t", "s_and_b32 %[rec], %[rec], 0xffff\n\t")
+        ".Ltbw_2%=:\n\t" TBW_HEAD TBW_MOVE TBW_NEXT("s_or_b32 %[li], %[li], 32\n\t", "s_lshr_b32 %[rec], %[rec], 16\n\t")
+        ".Ltbw_3%=:\n\t" TBW_HEAD
+        "s_cmp_eq_u32 %[m0], 0\n\t"
+        "s_cbranch_scc1 .Ltbw_slow%=\n\t" TBW_MOVE
+        "s_mov_b32 %[st], 0\n\t"
+        "s_branch .Ltbw_end%=\n"
+        ".Ltbw_slow%=:\n\t"
+        "s_mov_b32 %[st], 1\n\t"
+        "s_branch .Ltbw_end%=\n"
+        ".Ltbw_out%=:\n\t"
+        "s_mov_b32 %[st], 2\n"
+        ".Ltbw_end%=:"
+        : [r] "+s"(r), [j] "+s"(j), [rec] "+s"(rec), [vev] "+v"(vev), [st] "=s"(st), [t] "=&s"(t), [li] "=&s"(li),
+          [m0] "=&{m0}"(m0v)
+        : [k] "s"(k), [base] "s"(base), [win] "v"(win)
+        : "scc");
+    // (the divergence analysis takes inline-asm results as divergent: without
+    // these, everything downstream of r / j would go to VGPRs and exec masks)
+    r = uni(r), j = uni(j), rec = uni(rec), st = uni(st);
+#undef TBW_HEAD
+#undef TBW_MOVE
+#undef TBW_NEXT
+}
+
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
     const uint32_t lane = lane_id();
@@ -1289,13 +1363,20 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     const uint32_t *poff = G_poff(z, z.cur);
     const uint32_t *pred = G_pred(z, z.cur);
     const uint8_t *lds8 = reinterpret_cast<const uint8_t *>(z.lds);
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
     unsigned long long t_prev = stamp();
+    unsigned long long tq = t_prev;
+#define TB_MARK(slot)                     \
+    do {                                  \
+        const unsigned long long t_ = stamp(); \
+        z.pf[slot] += t_ - tq;            \
+        tq = t_;                          \
+    } while (0)
 #endif
     // stage the block holding row r (a switch to the prefetched neighbour
     // waits only for its DMA)
     auto to_block = [&]() {
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
         z.pf[kPfTbNsw] += 1;
         const unsigned long long ts0 = stamp();
 #endif
@@ -1315,7 +1396,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             pend = -1;
         }
         if (bi) tb_dma(z, bi - 1, buf ^ 1u);
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
         const unsigned long long ts1 = stamp();
         z.pf[kPfTbSwitch] += ts1 - ts0;
         t_prev += ts1 - ts0;
@@ -1333,6 +1414,14 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         return rec_at();
     };
     auto emit = [&](uint32_t e) { vev = (uint32_t)writelane((int)vev, (int)e, j & 63); };
+    // the record window of columns [jwv - 4, jwv) of the staged block (layout
+    // at vrot32 above); the compiler's lgkmcnt wait lands at the first use
+    auto tb_win = [&](int32_t jwv) -> uint32_t {
+        const uint32_t a = vrot32 + 2u * (uint32_t)(jwv - 1);
+        const uint32_t lo = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | (a & 255u)));
+        const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | ((a - 2u) & 255u)));
+        return lo | hi << 16;
+    };
     // j -= 1, handing a completed 64-base chunk to the store queue
     auto step_j = [&]() {
         if ((j & 63) == 0) {
@@ -1366,49 +1455,94 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             err = kErrTrace;
             break;
         }
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
         z.pf[kPfSpare0] += 1;
 #endif
         const uint32_t hc = rec & 3u;
-        if (hc == HC_MPRED) {  // state H
-            // plain steps while the next cell is in the block, the row not
-            // far, no chunk completes and no diagonal run starts
-            for (;;) {
-                emit((EV_ALN << 30) | r);
-                const uint32_t tag = (rec >> 4) & 63u;
-                const uint32_t li = r - base;
-#ifdef CCSX_TB_NOWIN
-                const uint32_t slow = ((farm >> li) & 1u) | ((j & 63) == 0 ? 1u : 0u) | (tag >= li ? 1u : 0u) |
-                                      ((rec & 0x3F3u) == 0x10u ? 1u : 0u);
-#else
-                // sign-bit arithmetic keeps the test on the scalar unit (a
-                // compare of a bool lowers to VALU selects): far row, a chunk
-                // completes ((j & 63) == 0), or the predecessor leaves the block
-                const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag - 1u) >> 31)) & 1u;
-#endif
-                if (slow) break;
-                --j;
-                r -= tag;
-#ifdef CCSX_TB_NOWIN
-                rec = rec_at();
-#else
-                // r stays inside the block (tag < li): the next record comes
-                // from the window by one readlane; an LDS round trip only
-                // every fourth column
-                uint32_t k = (uint32_t)(jw - 1 - j);
-                if (k >= 4u) {
-                    const uint32_t a = vrot32 + 2u * (uint32_t)j;
-                    const uint32_t lo = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | (a & 255u)));
-                    const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | ((a - 2u) & 255u)));
-                    win = lo | hi << 16;
-                    jw = j + 1, k = 0;
-                }
-                rec = ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((k & 2u) << 4))) >>
-                       ((k & 1u) * 16u)) & 0xFFFFu;
-#endif
-                if ((rec & 3u) != HC_MPRED) break;
+        bool emitted = false;  // (r, j) MPRED, emitted by the window steps: its move is pending
+#if !defined(CCSX_TB_NOWIN) && !defined(CCSX_TB_WIN1)
+        if (hc == HC_MPRED && farm == 0u) {
+            // A block without far rows: plain steps through 4-column windows
+            // aligned to jw = 0 mod 4 (tb_w4_steps), the next window read
+            // from LDS while this one is walked.
+            uint32_t k = (uint32_t)(jw - 1 - j);
+            if (k >= 4u) {
+                jw = (j & ~3) + 4;
+                win = tb_win(jw);
+                k = (uint32_t)(jw - 1 - j);
             }
-            if ((rec & 3u) != HC_MPRED) continue;
+            uint32_t wnx = tb_win(jw - 4);
+            uint32_t st;
+#ifdef CCSX_TB_COUNTING
+            const int32_t jin = j;
+            TB_MARK(kPfRowE);
+            z.pf[kPfRowA] += 1;
+#endif
+            for (;;) {
+                tb_w4_steps(k, base, win, r, j, rec, vev, st);
+                if (st) break;
+                win = wnx;
+                jw -= 4;
+                wnx = tb_win(jw - 4);
+                rec = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(r - base)) & 0xFFFFu;
+                if (rec & 3u) {
+                    st = 2;
+                    break;
+                }
+                k = 0;
+            }
+#ifdef CCSX_TB_COUNTING
+            z.pf[kPfRowB] += (uint32_t)(jin - j);
+            z.pf[kPfRowC] += st == 1 ? 1u : 0u;
+            TB_MARK(kPfTbStep);
+#endif
+            if (st == 2) continue;  // a D / I / MSRC record at the new (r, j)
+            emitted = true;
+        }
+#endif
+        if (hc == HC_MPRED) {  // state H
+            if (!emitted) {
+                // plain steps while the next cell is in the block, the row not
+                // far, no chunk completes and no diagonal run starts
+                for (;;) {
+                    emit((EV_ALN << 30) | r);
+                    const uint32_t tag = (rec >> 4) & 63u;
+                    const uint32_t li = r - base;
+#ifdef CCSX_TB_NOWIN
+                    const uint32_t slow = ((farm >> li) & 1u) | ((j & 63) == 0 ? 1u : 0u) | (tag >= li ? 1u : 0u) |
+                                          ((rec & 0x3F3u) == 0x10u ? 1u : 0u);
+#else
+                    // sign-bit arithmetic keeps the test on the scalar unit (a
+                    // compare of a bool lowers to VALU selects): far row, a chunk
+                    // completes ((j & 63) == 0), or the predecessor leaves the block
+                    const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag - 1u) >> 31)) & 1u;
+#endif
+                    if (slow) break;
+                    --j;
+                    r -= tag;
+#ifdef CCSX_TB_NOWIN
+                    rec = rec_at();
+#else
+                    // r stays inside the block (tag < li): the next record comes
+                    // from the window by one readlane; an LDS round trip only
+                    // every fourth column
+                    uint32_t k = (uint32_t)(jw - 1 - j);
+                    if (k >= 4u) {
+#ifdef CCSX_TB_WIN1
+                        jw = j + 1;
+#else
+                        jw = (j & ~3) + 4;  // aligned, as the unrolled loop above assumes
+#endif
+                        win = tb_win(jw);
+                        k = (uint32_t)(jw - 1 - j);
+                    }
+                    rec = ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((k & 2u) << 4))) >>
+                           ((k & 1u) * 16u)) & 0xFFFFu;
+#endif
+                    if ((rec & 3u) != HC_MPRED) break;
+                }
+                if ((rec & 3u) != HC_MPRED) continue;
+            }
             bool probed = false;
             if ((rec & 0x3F3u) == 0x10u && !((farm >> (r - base)) & 1u) && (j & 63) != 0 && r > base) {
                 // diagonal run: lane i checks that cell (r-1-i, j-1-i) is MPRED to
@@ -1431,7 +1565,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4u), (int)val);
                 const int32_t b = chunk + (int32_t)lane;
                 if (b <= j - 1 && b > j - 1 - (int32_t)k) vev = got;
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
                 z.pf[kPfSpare1] += k;
                 z.pf[kPfRowD] += 1;
 #endif
@@ -1445,6 +1579,9 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             if (probed) DP_STAMP(kPfTbProbe);
             else DP_STAMP(kPfTbStep);
             (void)probed;
+#if defined(CCSX_TB_COUNT) && !defined(CCSX_DP_STAMPS)
+            TB_MARK(kPfTbProbe);
+#endif
             continue;
         }
         if (hc == HC_MSRC) {
@@ -1455,11 +1592,11 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         }
         if (hc == HC_DEL) {
             // state D: follow D tags while the cell's D extends its predecessor's D
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
             z.pf[kPfTbDruns] += 1;
 #endif
             for (;;) {
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
                 z.pf[kPfTbDsteps] += 1;
 #endif
                 const uint32_t ext = rec & 4u;
@@ -1468,14 +1605,17 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 if (!ext || ++guard > glim) break;
             }
             DP_STAMP(kPfTbDI);
+#if defined(CCSX_TB_COUNT) && !defined(CCSX_DP_STAMPS)
+            TB_MARK(kPfTbDI);
+#endif
             continue;
         }
         // state I: insertions along the row
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
         z.pf[kPfTbIruns] += 1;
 #endif
         for (;;) {
-#ifdef CCSX_DP_STAMPS
+#ifdef CCSX_TB_COUNTING
             z.pf[kPfTbIsteps] += 1;
 #endif
             emit((EV_INS << 30) | r);
@@ -1485,6 +1625,9 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             if (!ext || ++guard > glim) break;
         }
         DP_STAMP(kPfTbDI);
+#if defined(CCSX_TB_COUNT) && !defined(CCSX_DP_STAMPS)
+        TB_MARK(kPfSpare2);
+#endif
     }
     if (err) {
         z.status = err;
