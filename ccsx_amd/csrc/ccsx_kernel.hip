@@ -956,8 +956,31 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     if (__builtin_expect(np == 1 && (uint32_t)(sh + 3) <= 7u && !(info & kInfoFar), 1)) {
         // one predecessor in the padded band: its H at t-1, t, t+1; D-ext is
         // D > H + O + E (D = max(H + O + E, D' + E))
-        const int32_t *b = z.lds + kLdsRing + (p0 % kRingA) * kRowW + (kHc - 1) + c.L2 + sh;
+        const int32_t *row = z.lds + kLdsRing + (p0 % kRingA) * kRowW;
+        const int32_t *b = row + (kHc - 1) + c.L2 + sh;  // cell 2l + sh - 1
+#ifndef CCSX_HELPER_B64
+        // three ds_read_b32 at a 2-word lane stride: a 2-way bank conflict
+        // each.  (Variant CCSX_HELPER_B64 -- one aligned ds_read_b64 per lane,
+        // the third cell by DPP -- cut SQ_LDS_BANK_CONFLICT 1.54e9 -> 1.12e9
+        // per launch but ran 1.5 % slower: the parity branch and edge-lane
+        // read cost the near-critical helpers more; tools/gpu_lds_ab.sh r02y)
         const int32_t hA = b[0], hB = b[1], hC = b[2];
+#else
+        // one 8-byte-aligned pair per lane (consecutive 8 B across the lanes:
+        // no LDS bank conflict) and the third cell from the neighbour lane by
+        // DPP.  The edge lane's cell (lane 63: 127 + sh, lane 0: sh - 1) is
+        // the pad -inf for the usual shifts 0 / 1, one broadcast read else.
+        int32_t hA, hB, hC;
+        if (sh & 1) {  // cell 2l + sh - 1 even: (hA, hB) aligned
+            const int2 v = *reinterpret_cast<const int2 *>(b);
+            const int32_t e = sh < 0 ? row[kHc + kW - 1 + sh] : kNegH;
+            hA = v.x, hB = v.y, hC = wave_shl1(e, v.x);
+        } else {  // (hB, hC) aligned
+            const int2 v = *reinterpret_cast<const int2 *>(b + 1);
+            const int32_t e = sh > 0 ? row[kHc + sh - 1] : kNegH;
+            hB = v.x, hC = v.y, hA = wave_shr1(e, v.y);
+        }
+#endif
         A.Mh0 = hA, A.Mh1 = hB;
         A.ms0 = A.ms1 = A.ds0 = A.ds1 = r - p0;
         A.dx0 = A.Dv0 > hB + (kO + kE) ? 4u : 0u;
