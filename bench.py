@@ -202,8 +202,19 @@ def main():
         dist.init_process_group("gloo")
 
     import ccsx_amd as cx
+    import ccsx_amd.native as nat
     zs = make_batch(cfg, rank)
-    eng = cx.Engine(local)
+    # one rank per GPU; with more local ranks than visible GPUs (rehearsing
+    # N > 1 on a one-GPU box) ranks share devices round-robin, each with its
+    # share of the device memory
+    ndev = nat.device_count()
+    if ndev <= 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    eng = cx.Engine(local % ndev)
+    sharing = (local_world + ndev - 1) // ndev
+    if sharing > 1:
+        eng.set_mem_share(sharing)
     eng.stage(zs)
     for _ in range(args.warmup):
         eng.launch(cfg["mode"])
@@ -262,6 +273,9 @@ def main():
                          "ops_per_cell": OPS_PER_CELL},
             "step_ms": [round(k, 3) for k in kernel_ms],
         }
+        if sharing > 1:
+            # a rehearsal, not a multi-GPU number: ranks share one device
+            out["config"]["ranks_per_device"] = sharing
     if args.e2e_zmws:
         e2e = e2e_line(eng, rank, args.e2e_zmws, dist)
     if rank == 0:

@@ -255,6 +255,11 @@ class SynthBatch:
 
 
 # ---------------------------------------------------------------- GPU engine
+def device_count() -> int:
+    """Visible HIP devices (0 without a GPU)."""
+    return int(lib().ccsx_gpu_device_count())
+
+
 class GpuError(RuntimeError):
     pass
 
@@ -338,6 +343,12 @@ class Engine:
         if rc != 0:
             self._err("ccsx_gpu_run")
         return [(out[i].status, out[i].cells, out[i].len) for i in range(batch.n)]
+
+    def set_mem_share(self, share: int) -> None:
+        """This context uses at most 1/share of the device's memory (several
+        contexts, or processes, on one device)."""
+        if self._L.ccsx_gpu_set_mem_share(self._ctx, share) != 0:
+            self._err("ccsx_gpu_set_mem_share")
 
     def set_kernel_cfg(self, cfg: int) -> None:
         """-1 = by slice size, 0 = latency (8-row blocks), 1 = occupancy (4-row blocks)."""

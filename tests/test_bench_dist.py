@@ -48,3 +48,39 @@ def test_rank_holes_disjoint():
 
 def test_single_rank_aggregate():
     assert bench.aggregate(None, 1.5, 7) == (1.5, 7.0)
+
+
+def _run_bench(nproc: int, extra: list[str]):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
+           "--gpus", str(nproc)] + extra
+    r = subprocess.run(cmd, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only prints
+    return json.loads(lines[0])
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_device():
+    """The driver's N > 1 launch (torch.distributed.run, one process per rank,
+    RANK/LOCAL_RANK/WORLD_SIZE from the env) with both ranks on the box's one
+    GPU: per-rank hole ranges, barrier, max-over-ranks time, summed cells, one
+    JSON line, and the e2e line's gather."""
+    small = ["--steps", "2", "--warmup", "1", "--nzmw", "96", "--e2e-zmws", "64", "--no-cpu-baseline"]
+    one = _run_bench(1, small)
+    two = _run_bench(2, small)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["config"].get("ranks_per_device", 1) >= 1
+    # rank 1 aligns its own 96 holes: the summed cells are two ranks' worth,
+    # and the two ranks' cell counts differ (disjoint synthetic holes)
+    assert two["cells_per_step"] > one["cells_per_step"]
+    assert two["cells_per_step"] != 2 * one["cells_per_step"]
+    assert two["value"] > 0 and two["e2e"]["value"] > 0
