@@ -47,7 +47,37 @@ __device__ __forceinline__ int dpp(int old, int v)
     return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, BM, false);
 }
 
-// inclusive max-scan over the 64 lanes: six in-place DPP max ops (a lane
+// inclusive max-scan over the 64 lanes: six DPP max steps (a lane whose DPP
+// source is out of range, or whose row is masked, keeps its own value).  Each
+// step is max(v, dpp(INT_MIN, v)): with the max's identity as the DPP mov's
+// old value the compiler folds the mov into one v_max_i32_dpp and, unlike an
+// asm block, fills the VALU-write -> DPP-read wait states with independent
+// work of the row instead of s_nop (CCSX_ASM_SCAN: the hand-written form).
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ int dpp_max(int v)
+{
+    return max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, CTRL, RM, 0xF, false));
+}
+
+#ifndef CCSX_ASM_SCAN
+__device__ __forceinline__ int wave_incl_max(int v)
+{
+    v = dpp_max<0x111>(v);
+    v = dpp_max<0x112>(v);
+    v = dpp_max<0x114>(v);
+    v = dpp_max<0x118>(v);
+    v = dpp_max<0x142, 0xA>(v);
+    return dpp_max<0x143, 0xC>(v);
+}
+
+// two independent inclusive max-scans (interleaved by the scheduler)
+__device__ __forceinline__ void wave_incl_max2(int &a, int &b)
+{
+    a = wave_incl_max(a);
+    b = wave_incl_max(b);
+}
+#else
+// (hand-written form) inclusive max-scan: six in-place DPP max ops (a lane
 // whose DPP source is out of range, or whose row is masked, is not written,
 // i.e. keeps its own value).  Hand-written because hipcc does not fold the
 // DPP movs into the max; the s_nop 1 cover the VALU-write -> DPP-read hazard.
@@ -96,6 +126,8 @@ __device__ __forceinline__ void wave_incl_max2(int &a, int &b)
         "s_nop 1"
         : "+v"(a), "+v"(b));
 }
+
+#endif
 
 __device__ __forceinline__ int wave_incl_sum(int v)
 {
