@@ -1304,19 +1304,92 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
 }
 
 // Plain MPRED steps k..3 of an aligned 4-column record window (traceback;
-// columns jw - 1 .. jw - 4 of the staged block's 32 rows, layout at vrot32):
-// per step, emit ALN | r at lane j & 63; leave with st = 1, unmoved, when the
+// columns jw - 1 .. jw - 4 of the staged block's 32 rows): wa holds, at lane
+// l < 32 = block row l, columns jw - 1 (low half) and jw - 2 (high half), wb
+// columns jw - 3 and jw - 4 (tb_win's upper 32 lanes moved down by one
+// v_permlane32_swap), so every step reads its record at lane r - base.  Per
+// step, emit ALN | r at lane j & 63; leave with st = 1, unmoved, when the
 // cell's predecessor lies outside the block (tag >= r - base) or, on the
 // window's last column (j = 0 mod 4), when j completes a 64-base chunk; else
-// j -= 1, r -= tag and, below the last column, read the next record from the
-// window (lane (r - base) + 32 for columns 2 and 3, low / high half for even
-// / odd columns) and leave with st = 2 when it is not MPRED.  st = 0: moved
-// past the last column (the caller swaps in the next window).  Hand-written:
-// compiled, the multi-exit unrolled loop became a flag-driven state machine
-// of ~35 scalar instructions per step; here a step is 14.  (Measured: the
-// walk is latency-bound, ~150 cycles per step either way; this form is 0.3 %
-// faster per launch.  Handling D / I steps inside the window as well measured
-// no faster: tools/gpu_ab.sh r02u.)
+// j -= 1, r -= tag and, below the last column, read the next record and leave
+// with st = 2 when it is not MPRED.  st = 0: moved past the last column (the
+// caller swaps in the next window).  The walk keeps li = r - base as its own
+// variable and leaves high-half records in place (their tag and code are read
+// at bit 20 / 16), so the dependent chain of a step is s_bfe -> s_sub ->
+// v_readlane; a step is 11 instructions.  (CCSX_TB_W64: the previous form,
+// one 64-lane window, li recomputed and the half shifted down per step, 14.)
+// Hand-written: compiled, the multi-exit unrolled loop became a flag-driven
+// state machine of ~35 scalar instructions per step.  (Handling D / I steps
+// inside the window as well measured no faster: tools/gpu_ab.sh r02u.)
+#ifndef CCSX_TB_W64
+__device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t wa, uint32_t wb, uint32_t &r,
+                                            int32_t &j, uint32_t &rec, uint32_t &vev, uint32_t &st)
+{
+    uint32_t t, li, c, m0v;
+    // the asm's scalar operands must live in SGPRs
+    r = uni(r), j = uni(j), rec = uni(rec), k = uni(k), base = uni(base);
+#define TBW_HEAD(BFE, SLOW)                              \
+    "s_and_b32 %[m0], %[j], 63\n\t"                      \
+    "v_writelane_b32 %[vev], %[r], %[m0]\n\t"            \
+    "s_bfe_u32 %[t], %[rec], " BFE "\n\t"                \
+    "s_cmp_ge_u32 %[t], %[li]\n\t"                       \
+    "s_cbranch_scc1 .Ltbw_" SLOW "%=\n\t"
+#define TBW_MOVE                                         \
+    "s_sub_u32 %[j], %[j], 1\n\t"                        \
+    "s_sub_u32 %[li], %[li], %[t]\n\t"                   \
+    "s_sub_u32 %[r], %[r], %[t]\n\t"
+#define TBW_NEXT(W, CODE, OUT)                           \
+    "v_readlane_b32 %[rec], %[" W "], %[li]\n\t"         \
+    "s_and_b32 %[c], %[rec], " CODE "\n\t"               \
+    "s_cbranch_scc1 .Ltbw_" OUT "%=\n\t"
+    asm volatile(
+        "s_sub_u32 %[li], %[r], %[base]\n\t"
+        "s_cmp_eq_u32 %[k], 0\n\t"
+        "s_cbranch_scc1 .Ltbw_0%=\n\t"
+        "s_cmp_eq_u32 %[k], 2\n\t"
+        "s_cbranch_scc1 .Ltbw_2%=\n\t"
+        "s_lshl_b32 %[rec], %[rec], 16\n\t"  // k = 1 or 3: a high-half column
+        "s_cmp_eq_u32 %[k], 1\n\t"
+        "s_cbranch_scc1 .Ltbw_1%=\n\t"
+        "s_branch .Ltbw_3%=\n"
+        ".Ltbw_0%=:\n\t" TBW_HEAD("0x60004", "slowlo") TBW_MOVE TBW_NEXT("wa", "0x30000", "outhi")
+        ".Ltbw_1%=:\n\t" TBW_HEAD("0x60014", "slowhi") TBW_MOVE TBW_NEXT("wb", "3", "outlo")
+        ".Ltbw_2%=:\n\t" TBW_HEAD("0x60004", "slowlo") TBW_MOVE TBW_NEXT("wb", "0x30000", "outhi")
+        ".Ltbw_3%=:\n\t" TBW_HEAD("0x60014", "slowhi")
+        "s_cmp_eq_u32 %[m0], 0\n\t"
+        "s_cbranch_scc1 .Ltbw_slowhi%=\n\t" TBW_MOVE
+        "s_mov_b32 %[st], 0\n\t"
+        "s_branch .Ltbw_end%=\n"
+        ".Ltbw_slowhi%=:\n\t"
+        "s_lshr_b32 %[rec], %[rec], 16\n"
+        ".Ltbw_slowlo%=:\n\t"
+        "s_mov_b32 %[st], 1\n\t"
+        "s_branch .Ltbw_clean%=\n"
+        ".Ltbw_outhi%=:\n\t"
+        "s_lshr_b32 %[rec], %[rec], 16\n"
+        ".Ltbw_outlo%=:\n\t"
+        "s_mov_b32 %[st], 2\n"
+        ".Ltbw_clean%=:\n\t"
+        "s_and_b32 %[rec], %[rec], 0xffff\n"
+        ".Ltbw_end%=:"
+        : [r] "+s"(r), [j] "+s"(j), [rec] "+s"(rec), [vev] "+v"(vev), [st] "=s"(st), [t] "=&s"(t), [li] "=&s"(li),
+          [c] "=&s"(c), [m0] "=&{m0}"(m0v)
+        : [k] "s"(k), [base] "s"(base), [wa] "v"(wa), [wb] "v"(wb)
+        : "scc");
+    // (the divergence analysis takes inline-asm results as divergent: without
+    // these, everything downstream of r / j would go to VGPRs and exec masks)
+    r = uni(r), j = uni(j), rec = uni(rec), st = uni(st);
+#undef TBW_HEAD
+#undef TBW_MOVE
+#undef TBW_NEXT
+}
+
+// the lower 32 lanes of wb <- the upper 32 lanes of the 64-lane window
+__device__ __forceinline__ uint32_t tb_wb(uint32_t win)
+{
+    return (uint32_t)__builtin_amdgcn_permlane32_swap(win, win, false, false)[1];
+}
+#else
 __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t win, uint32_t &r, int32_t &j,
                                             uint32_t &rec, uint32_t &vev, uint32_t &st)
 {
@@ -1371,6 +1444,7 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
 #undef TBW_MOVE
 #undef TBW_NEXT
 }
+#endif
 
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
@@ -1534,7 +1608,11 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             z.pf[kPfRowA] += 1;
 #endif
             for (;;) {
+#ifndef CCSX_TB_W64
+                tb_w4_steps(k, base, win, tb_wb(win), r, j, rec, vev, st);
+#else
                 tb_w4_steps(k, base, win, r, j, rec, vev, st);
+#endif
                 if (st) break;
                 win = wnx;
                 jw -= 4;
