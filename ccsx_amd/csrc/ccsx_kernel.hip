@@ -168,6 +168,16 @@ __device__ __forceinline__ int writelane(int v, int x, int l)
     return v;
 }
 
+#ifdef CCSX_WL_NV
+__device__ __forceinline__ int writelane_nv(int v, int x, int l)
+{
+    asm("v_writelane_b32 %0, %1, %2"
+        : "+v"(v)
+        : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(__builtin_amdgcn_readfirstlane(l)));
+    return v;
+}
+#endif
+
 __device__ __forceinline__ int wave_max(int v) { return __builtin_amdgcn_readlane(wave_incl_max(v), 63); }
 
 __device__ __forceinline__ int wave_min(int v) { return -wave_max(-v); }
@@ -804,8 +814,16 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
         // (inline asm measured 0.6 % faster than the compiler's writelane
         // intrinsic here: it keeps vOff / vKey out of the scheduler's way)
+#if defined(CCSX_WL_BUILTIN)
+        S.vOff = __builtin_amdgcn_writelane(off, li, S.vOff);
+        S.vKey = __builtin_amdgcn_writelane(key, li, S.vKey);
+#elif defined(CCSX_WL_NV)
+        S.vOff = writelane_nv(S.vOff, off, li);
+        S.vKey = writelane_nv(S.vKey, key, li);
+#else
         S.vOff = writelane(S.vOff, off, li);
         S.vKey = writelane(S.vKey, key, li);
+#endif
         if (cold && (info & kInfoSpill)) {
             // a successor lies beyond the ring: keep this row in HBM
             const uint32_t sl = S.nspill++;
@@ -1464,6 +1482,9 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     // valid while j lies in [jw - 4, jw) (entering a block invalidates it)
     uint32_t vrot32 = 0, rowb32 = 0, win = 0;
     int32_t jw = INT32_MIN / 2;
+    // the window below it (columns [jw - 8, jw - 4)), valid while jwn == jw
+    uint32_t wnx = 0;
+    int32_t jwn = INT32_MAX;
     auto enter = [&]() {
         const uint32_t mt = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
         voff = mt & 0x7FFFFFFFu;
@@ -1472,6 +1493,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         vrot32 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & 31u) * 4u), (int)vrot) - ((lane >> 5) * 4u);
         rowb32 = (buf * 32u + (lane & 31u)) << 8;
         jw = INT32_MIN / 2;
+        jwn = INT32_MAX;
     };
     tb_dma(z, bi, buf);
     __builtin_amdgcn_s_waitcnt(0);
@@ -1542,6 +1564,23 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         if (r < base) to_block();
         return rec_at();
     };
+    // the record of cell (r, j) from the current 4-column window by one
+    // readlane when j lies in it (D / I steps), else from LDS; r must lie in
+    // the staged block
+    auto rec_win = [&]() -> uint32_t {
+#ifndef CCSX_TB_DI_LDS
+        const uint32_t kk = (uint32_t)(jw - 1 - j);
+        if (kk < 4u)
+            return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
+                    ((kk & 1u) * 16u)) & 0xFFFFu;
+#ifndef CCSX_TB_NO_WNX
+        if (kk < 8u && jwn == jw)
+            return ((uint32_t)__builtin_amdgcn_readlane((int)wnx, (int)((r - base) + ((kk & 2u) << 4))) >>
+                    ((kk & 1u) * 16u)) & 0xFFFFu;
+#endif
+#endif
+        return rec_at();
+    };
     auto emit = [&](uint32_t e) { vev = (uint32_t)writelane((int)vev, (int)e, j & 63); };
     // the record window of columns [jwv - 4, jwv) of the staged block (layout
     // at vrot32 above); the compiler's lgkmcnt wait lands at the first use
@@ -1596,11 +1635,22 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             // from LDS while this one is walked.
             uint32_t k = (uint32_t)(jw - 1 - j);
             if (k >= 4u) {
-                jw = (j & ~3) + 4;
-                win = tb_win(jw);
+#ifndef CCSX_TB_NO_WNX
+                if (jwn == jw && k < 8u) {
+                    win = wnx;  // j moved into the window below (already read)
+                    jw -= 4;
+                } else
+#endif
+                {
+                    jw = (j & ~3) + 4;
+                    win = tb_win(jw);
+                }
                 k = (uint32_t)(jw - 1 - j);
             }
-            uint32_t wnx = tb_win(jw - 4);
+            if (jwn != jw) {
+                wnx = tb_win(jw - 4);
+                jwn = jw;
+            }
             uint32_t st;
 #ifdef CCSX_TB_COUNTING
             const int32_t jin = j;
@@ -1617,6 +1667,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 win = wnx;
                 jw -= 4;
                 wnx = tb_win(jw - 4);
+                jwn = jw;
                 rec = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(r - base)) & 0xFFFFu;
                 if (rec & 3u) {
                     st = 2;
@@ -1708,7 +1759,8 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             }
             step_j();
             to_pred((rec >> 4) & 63u, j + 1, 0u);  // the MPRED cell is (r, j + 1)
-            rec = cell();
+            if (r < base) to_block();
+            rec = rec_win();
             if (probed) DP_STAMP(kPfTbProbe);
             else DP_STAMP(kPfTbStep);
             (void)probed;
@@ -1734,7 +1786,8 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
 #endif
                 const uint32_t ext = rec & 4u;
                 to_pred((rec >> 10) & 63u, j, 1u);
-                rec = cell();
+                if (r < base) to_block();
+                rec = rec_win();
                 if (!ext || ++guard > glim) break;
             }
             DP_STAMP(kPfTbDI);
@@ -1754,7 +1807,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             emit((EV_INS << 30) | r);
             const uint32_t ext = rec & 8u;
             step_j();
-            rec = rec_at();
+            rec = rec_win();
             if (!ext || ++guard > glim) break;
         }
         DP_STAMP(kPfTbDI);
