@@ -1560,28 +1560,6 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                            (((uint32_t)__builtin_amdgcn_readlane((int)vrot, (int)li) + 2u * (uint32_t)j) & 255u);
         return uni((uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + a));
     };
-    auto cell = [&]() -> uint32_t {
-        if (r < base) to_block();
-        return rec_at();
-    };
-    // the record of cell (r, j) from the current 4-column window by one
-    // readlane when j lies in it (D / I steps), else from LDS; r must lie in
-    // the staged block
-    auto rec_win = [&]() -> uint32_t {
-#ifndef CCSX_TB_DI_LDS
-        const uint32_t kk = (uint32_t)(jw - 1 - j);
-        if (kk < 4u)
-            return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
-                    ((kk & 1u) * 16u)) & 0xFFFFu;
-#ifndef CCSX_TB_NO_WNX
-        if (kk < 8u && jwn == jw)
-            return ((uint32_t)__builtin_amdgcn_readlane((int)wnx, (int)((r - base) + ((kk & 2u) << 4))) >>
-                    ((kk & 1u) * 16u)) & 0xFFFFu;
-#endif
-#endif
-        return rec_at();
-    };
-    auto emit = [&](uint32_t e) { vev = (uint32_t)writelane((int)vev, (int)e, j & 63); };
     // the record window of columns [jwv - 4, jwv) of the staged block (layout
     // at vrot32 above); the compiler's lgkmcnt wait lands at the first use
     auto tb_win = [&](int32_t jwv) -> uint32_t {
@@ -1590,6 +1568,36 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | ((a - 2u) & 255u)));
         return lo | hi << 16;
     };
+    // the record of cell (r, j) from the current 4-column window, or the one
+    // below it, by one readlane; else the window holding column j is read
+    // (one LDS round trip, which the window steps then reuse); r must lie in
+    // the staged block
+    auto rec_win = [&]() -> uint32_t {
+#ifndef CCSX_TB_DI_LDS
+        uint32_t kk = (uint32_t)(jw - 1 - j);
+        if (kk < 4u)
+            return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
+                    ((kk & 1u) * 16u)) & 0xFFFFu;
+#ifndef CCSX_TB_NO_WNX
+        if (kk < 8u && jwn == jw)
+            return ((uint32_t)__builtin_amdgcn_readlane((int)wnx, (int)((r - base) + ((kk & 2u) << 4))) >>
+                    ((kk & 1u) * 16u)) & 0xFFFFu;
+#endif
+#ifndef CCSX_TB_REC_LDS
+        jw = (j & ~3) + 4;
+        win = tb_win(jw);
+        kk = (uint32_t)(jw - 1 - j);
+        return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
+                ((kk & 1u) * 16u)) & 0xFFFFu;
+#endif
+#endif
+        return rec_at();
+    };
+    auto cell = [&]() -> uint32_t {
+        if (r < base) to_block();
+        return rec_win();
+    };
+    auto emit = [&](uint32_t e) { vev = (uint32_t)writelane((int)vev, (int)e, j & 63); };
     // j -= 1, handing a completed 64-base chunk to the store queue
     auto step_j = [&]() {
         if ((j & 63) == 0) {
