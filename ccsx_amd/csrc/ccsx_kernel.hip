@@ -1340,6 +1340,13 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
 // state machine of ~35 scalar instructions per step.  (Handling D / I steps
 // inside the window as well measured no faster: tools/gpu_ab.sh r02u.)
 #ifndef CCSX_TB_W64
+// leave the window walk when the predecessor row lies below the block
+// (tag > li; CCSX_TB_GE: also when it is the block's first row)
+#ifdef CCSX_TB_GE
+#define TBW_LEAVE "s_cmp_ge_u32 %[t], %[li]\n\t"
+#else
+#define TBW_LEAVE "s_cmp_gt_u32 %[t], %[li]\n\t"
+#endif
 __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t wa, uint32_t wb, uint32_t &r,
                                             int32_t &j, uint32_t &rec, uint32_t &vev, uint32_t &st)
 {
@@ -1350,7 +1357,7 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
     "s_and_b32 %[m0], %[j], 63\n\t"                      \
     "v_writelane_b32 %[vev], %[r], %[m0]\n\t"            \
     "s_bfe_u32 %[t], %[rec], " BFE "\n\t"                \
-    "s_cmp_ge_u32 %[t], %[li]\n\t"                       \
+    TBW_LEAVE                       \
     "s_cbranch_scc1 .Ltbw_" SLOW "%=\n\t"
 #define TBW_MOVE                                         \
     "s_sub_u32 %[j], %[j], 1\n\t"                        \
@@ -1707,7 +1714,11 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                     // sign-bit arithmetic keeps the test on the scalar unit (a
                     // compare of a bool lowers to VALU selects): far row, a chunk
                     // completes ((j & 63) == 0), or the predecessor leaves the block
+#ifdef CCSX_TB_GE
                     const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag - 1u) >> 31)) & 1u;
+#else
+                    const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag) >> 31)) & 1u;
+#endif
 #endif
                     if (slow) break;
                     --j;
@@ -1736,7 +1747,14 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 if ((rec & 3u) != HC_MPRED) continue;
             }
             bool probed = false;
+            // (CCSX_TB_PROBE: walk a run of tag-1 diagonal cells by one lane
+            // vector test here; with the windows it measured 0.3 % slower,
+            // A/B r02s9)
+#ifdef CCSX_TB_PROBE
             if ((rec & 0x3F3u) == 0x10u && !((farm >> (r - base)) & 1u) && (j & 63) != 0 && r > base) {
+#else
+            if (false) {
+#endif
                 // diagonal run: lane i checks that cell (r-1-i, j-1-i) is MPRED to
                 // the row above it, inside this block and this event chunk; the
                 // run's events go into vev by one lane permutation
