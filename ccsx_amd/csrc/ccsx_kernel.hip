@@ -1497,7 +1497,12 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         voff = mt & 0x7FFFFFFFu;
         vrot = (tb_rot(lane) - 2u * voff) & 255u;
         farm = (uint32_t)ballot((mt >> 31) != 0u);
+#ifdef CCSX_TB_BPERM
         vrot32 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & 31u) * 4u), (int)vrot) - ((lane >> 5) * 4u);
+#else
+        // lanes 32-63 take lane l - 32's rotation (v_permlane32_swap: no LDS)
+        vrot32 = (uint32_t)__builtin_amdgcn_permlane32_swap(vrot, vrot, false, false)[0] - ((lane >> 5) * 4u);
+#endif
         rowb32 = (buf * 32u + (lane & 31u)) << 8;
         jw = INT32_MIN / 2;
         jwn = INT32_MAX;
