@@ -407,7 +407,7 @@ constexpr int kPrioWave0 = CCSX_PRIO_WAVE0, kPrioMerge = CCSX_PRIO_MERGE;
 static_assert(kRingA >= kRing + 2 * kBlkAB, "B reads predecessors up to kRing rows behind its row");
 
 
-enum JobKind : int32_t { kJobExit = 0, kJobDp = 1, kJobMerge = 2 };
+enum JobKind : int32_t { kJobExit = 0, kJobDp = 1, kJobMerge = 2, kJobColumns = 3 };
 struct DpJob {
     int32_t kind;
     uint32_t m, R, cur;
@@ -1195,6 +1195,7 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
 
 template <bool LM>
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid);
+__device__ __forceinline__ void columns_count(const Z &z, uint32_t n, uint32_t ncols, uint32_t tid, uint32_t T);
 __device__ __forceinline__ bool merge_in_lds(uint32_t R);
 
 // helper wave h (1 + h = wave index): serve DP and merge jobs until wave 0
@@ -1210,6 +1211,12 @@ __device__ __forceinline__ void dp_helper(Z &z, uint32_t h)
         z.cur = uni((int)job->cur);
         z.status = kOk;
         const uint32_t m = uni(job->m);
+        if (kind == kJobColumns) {
+            __syncthreads();  // columns numbered by wave 0
+            columns_count(z, m, uni(job->K), threadIdx.x, kBlockThreads);
+            __syncthreads();
+            continue;
+        }
         if (kind == kJobMerge) {
             // merge's row-parallel phases are on the critical path: raise the
             // helpers above other workgroups' DP helpers (below any wave 0)
@@ -2232,37 +2239,18 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
 // ----------------------------------------------------------------------------
 // SPEC.md §6: columns, per-column consensus and the consensus-match masks
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
+// per-column base counts, consensus base, coverage and the consensus row's
+// read mask of columns tid, tid + T, ... (every wave of the workgroup)
+__device__ __forceinline__ void columns_count(const Z &z, uint32_t n, uint32_t ncols, uint32_t tid, uint32_t T)
 {
-    const uint32_t lane = lane_id();
-    const uint32_t R = z.R, nw = z.d.nw;
+    const uint32_t nw = z.d.nw;
     const uint8_t *nb = G_nb(z, z.cur);
     const uint64_t *mem = G_mem(z, z.cur);
-    uint32_t *colof = P<uint32_t>(z, z.L.colof);
-    uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
+    const uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
     uint8_t *cons = P<uint8_t>(z, z.L.cons);
     uint64_t *cmask = P<uint64_t>(z, z.L.cmask);
-    const uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
-    uint32_t *rfc = P<uint32_t>(z, z.L.rfc), *rlc = P<uint32_t>(z, z.L.rlc);
-    uint32_t carry = 0;
-    for (uint32_t r0 = 0; r0 < R; r0 += 64) {
-        const uint32_t r = r0 + lane;
-        const bool f = r < R && (nb[r] & 4);
-        const uint64_t bal = ballot(f);
-        const uint32_t c = carry + lanes_below(bal) + (f ? 1u : 0u) - 1u;
-        if (r < R) colof[r] = c;
-        if (f) colrow[c] = r;
-        carry += (uint32_t)__builtin_popcountll(bal);
-    }
-    const uint32_t ncols = carry;
-    if (lane == 0) colrow[ncols] = R;
-    wsync();
-    for (uint32_t k = lane; k < n; k += 64) {
-        rfc[k] = rfirst[k] != kNone ? colof[rfirst[k]] : kNone;
-        rlc[k] = rfirst[k] != kNone ? colof[rlast[k]] : 0u;
-    }
-    wsync();
-    for (uint32_t c = lane; c < ncols; c += 64) {
+    const uint32_t *rfc = P<uint32_t>(z, z.L.rfc), *rlc = P<uint32_t>(z, z.L.rlc);
+    for (uint32_t c = tid; c < ncols; c += T) {
         const uint32_t a = colrow[c], e = colrow[c + 1];
         uint32_t cnt[4] = {0, 0, 0, 0}, tot = 0, cov = 0;
         for (uint32_t u = a; u < e; ++u) {
@@ -2283,7 +2271,52 @@ __device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
             if ((nb[u] & 3u) == cb) crow = u;
         for (uint32_t w = 0; w < nw; ++w) cmask[(size_t)c * nw + w] = crow != kNone ? mem[(size_t)crow * nw + w] : 0ull;
     }
+}
+
+// Column numbering and the reads' first / last columns on wave 0, then the
+// per-column counts on all three waves (job kJobColumns: the helpers join at
+// the two barriers after the job barrier; CCSX_COLS_W0: wave 0 alone)
+__device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t R = z.R;
+    const uint8_t *nb = G_nb(z, z.cur);
+    uint32_t *colof = P<uint32_t>(z, z.L.colof);
+    uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
+    const uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
+    uint32_t *rfc = P<uint32_t>(z, z.L.rfc), *rlc = P<uint32_t>(z, z.L.rlc);
+#ifndef CCSX_COLS_W0
+    volatile DpJob *job = dp_job(z);
+    if (lane == 0) job->kind = kJobColumns, job->m = n, job->R = R, job->cur = (uint32_t)z.cur;
+    __syncthreads();  // J: job posted
+#endif
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < R; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        const bool f = r < R && (nb[r] & 4);
+        const uint64_t bal = ballot(f);
+        const uint32_t c = carry + lanes_below(bal) + (f ? 1u : 0u) - 1u;
+        if (r < R) colof[r] = c;
+        if (f) colrow[c] = r;
+        carry += (uint32_t)__builtin_popcountll(bal);
+    }
+    const uint32_t ncols = carry;
+    if (lane == 0) colrow[ncols] = R;
     wsync();
+    for (uint32_t k = lane; k < n; k += 64) {
+        rfc[k] = rfirst[k] != kNone ? colof[rfirst[k]] : kNone;
+        rlc[k] = rfirst[k] != kNone ? colof[rlast[k]] : 0u;
+    }
+#ifndef CCSX_COLS_W0
+    if (lane == 0) job->K = ncols;
+    __syncthreads();  // columns numbered, ncols posted
+    columns_count(z, n, ncols, threadIdx.x, kBlockThreads);
+    __syncthreads();  // every column counted
+#else
+    wsync();
+    columns_count(z, n, ncols, lane, 64);
+    wsync();
+#endif
     return ncols;
 }
 
