@@ -755,7 +755,8 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
 // cell is a read position; else (m < W, off == 0) cells t >= m are invalid:
 // H = kNegH, D = kNeg there, and they take no part in the row maximum.
 template <bool FULL>
-__device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim, uint32_t m, const LaneK &c)
+__device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim, uint32_t m, const LaneK &c,
+                                        uint32_t ring)
 {
     const int lane = lane_id();
 #ifdef CCSX_DP_STAMPS
@@ -809,7 +810,12 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         }
         const int32_t key = __builtin_amdgcn_readlane(rk, 63);
         // ring row, meta window
+#ifdef CCSX_RING_INC
+        (void)ring;
         int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + S.ring + kHc + c.L2);
+#else
+        int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
+#endif
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
         // (inline asm measured 0.6 % faster than the compiler's writelane
@@ -840,7 +846,9 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
         S.pOff = off;
         S.pArg = off + 127 - (key & 127);
+#ifdef CCSX_RING_INC
         S.ring = S.ring + kRowW == (uint32_t)(kRingA * kRowW) ? 0u : S.ring + kRowW;
+#endif
 #ifdef CCSX_DP_STAMPS
         if (!cold && ckind != 6) {
             ROW_STAMP(ts2);
@@ -928,11 +936,16 @@ __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t
         const uint32_t inf = S.W.cur.info;
         S.fmask = ballot((inf & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain);
     }
+    // ring slots of the block's rows: r0 is a multiple of kBlkAB, which
+    // divides kRingA, so the block's rows take consecutive slots (constant
+    // offsets from the block's first)
+    static_assert(kRingA % kBlkAB == 0, "a block's rows occupy consecutive ring slots");
+    const uint32_t rb = (r0 % (uint32_t)kRingA) * (uint32_t)kRowW;
     if (r0 + kBlkAB <= z.R) {
 #pragma unroll
-        for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c);
+        for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c, rb + i * kRowW);
     } else {
-        for (uint32_t i = 0; r0 + i < z.R; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c);
+        for (uint32_t i = 0; r0 + i < z.R; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c, rb + i * kRowW);
     }
     z.lds[kLdsOffRing + lane] = S.vOff;  // band offsets of the last 64 rows for the helpers
     recwin_end(S.W, r0);
@@ -1357,17 +1370,31 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
 __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t wa, uint32_t wb, uint32_t &r,
                                             int32_t &j, uint32_t &rec, uint32_t &vev, uint32_t &st)
 {
-    uint32_t t, li, c, m0v;
+    uint32_t t, li, c, jh, m0v;
     // the asm's scalar operands must live in SGPRs
     r = uni(r), j = uni(j), rec = uni(rec), k = uni(k), base = uni(base);
+#ifdef CCSX_TBW_JSUB
+#define TBW_M0 "s_and_b32 %[m0], %[j], 63\n\t"
+#define TBW_J "s_sub_u32 %[j], %[j], 1\n\t"
+#define TBW_ENTRY ""
+#define TBW_EXIT ""
+#else
+// m0 = j & 63 is kept by the walk (the window's columns never cross a
+// 64-base chunk: jw = 0 mod 4 and the last column leaves on a completed
+// chunk), j rebuilt from it at the exits
+#define TBW_M0 ""
+#define TBW_J "s_sub_u32 %[m0], %[m0], 1\n\t"
+#define TBW_ENTRY "s_and_b32 %[m0], %[j], 63\n\ts_andn2_b32 %[jh], %[j], 63\n\t"
+#define TBW_EXIT "s_or_b32 %[j], %[jh], %[m0]\n\t"
+#endif
 #define TBW_HEAD(BFE, SLOW)                              \
-    "s_and_b32 %[m0], %[j], 63\n\t"                      \
+    TBW_M0                                               \
     "v_writelane_b32 %[vev], %[r], %[m0]\n\t"            \
     "s_bfe_u32 %[t], %[rec], " BFE "\n\t"                \
     TBW_LEAVE                       \
     "s_cbranch_scc1 .Ltbw_" SLOW "%=\n\t"
 #define TBW_MOVE                                         \
-    "s_sub_u32 %[j], %[j], 1\n\t"                        \
+    TBW_J                                                \
     "s_sub_u32 %[li], %[li], %[t]\n\t"                   \
     "s_sub_u32 %[r], %[r], %[t]\n\t"
 #define TBW_NEXT(W, CODE, OUT)                           \
@@ -1375,7 +1402,7 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
     "s_and_b32 %[c], %[rec], " CODE "\n\t"               \
     "s_cbranch_scc1 .Ltbw_" OUT "%=\n\t"
     asm volatile(
-        "s_sub_u32 %[li], %[r], %[base]\n\t"
+        "s_sub_u32 %[li], %[r], %[base]\n\t" TBW_ENTRY
         "s_cmp_eq_u32 %[k], 0\n\t"
         "s_cbranch_scc1 .Ltbw_0%=\n\t"
         "s_cmp_eq_u32 %[k], 2\n\t"
@@ -1391,7 +1418,7 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
         "s_cmp_eq_u32 %[m0], 0\n\t"
         "s_cbranch_scc1 .Ltbw_slowhi%=\n\t" TBW_MOVE
         "s_mov_b32 %[st], 0\n\t"
-        "s_branch .Ltbw_end%=\n"
+        "s_branch .Ltbw_clean%=\n"
         ".Ltbw_slowhi%=:\n\t"
         "s_lshr_b32 %[rec], %[rec], 16\n"
         ".Ltbw_slowlo%=:\n\t"
@@ -1401,11 +1428,11 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
         "s_lshr_b32 %[rec], %[rec], 16\n"
         ".Ltbw_outlo%=:\n\t"
         "s_mov_b32 %[st], 2\n"
-        ".Ltbw_clean%=:\n\t"
+        ".Ltbw_clean%=:\n\t" TBW_EXIT
         "s_and_b32 %[rec], %[rec], 0xffff\n"
         ".Ltbw_end%=:"
         : [r] "+s"(r), [j] "+s"(j), [rec] "+s"(rec), [vev] "+v"(vev), [st] "=s"(st), [t] "=&s"(t), [li] "=&s"(li),
-          [c] "=&s"(c), [m0] "=&{m0}"(m0v)
+          [c] "=&s"(c), [jh] "=&s"(jh), [m0] "=&{m0}"(m0v)
         : [k] "s"(k), [base] "s"(base), [wa] "v"(wa), [wb] "v"(wb)
         : "scc");
     // (the divergence analysis takes inline-asm results as divergent: without
@@ -1414,6 +1441,10 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
 #undef TBW_HEAD
 #undef TBW_MOVE
 #undef TBW_NEXT
+#undef TBW_M0
+#undef TBW_J
+#undef TBW_ENTRY
+#undef TBW_EXIT
 }
 
 // the lower 32 lanes of wb <- the upper 32 lanes of the 64-lane window
