@@ -28,6 +28,7 @@ def main():
     write(fa, nz, L, passes)
     print(f"input: {nz} ZMWs, {os.path.getsize(fa) / 1e6:.1f} MB, written in {time.time() - t:.1f} s", flush=True)
     if not os.path.exists(IB):
+        os.makedirs(os.path.dirname(IB), exist_ok=True)  # (build/ does not travel to the GPU box)
         subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-I",
                         os.path.join(ROOT, "ccsx_amd", "csrc", "host"), os.path.join(ROOT, "tools", "ingest_bench.cpp"),
                         "-L", os.path.join(ROOT, "ccsx_amd"), "-lccsx_amd", "-lz", "-lpthread",
