@@ -296,12 +296,11 @@ __device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return ((uin
 // (off >> 1) + l holds, in nibble off & 1, the codes of read positions
 // off + 2l and off + 2l + 1 -- one ds_read_u8 per lane per DP row
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
+__device__ __forceinline__ void stage_read(const Z &z, const uint8_t *src, uint32_t m, uint32_t tid, uint32_t T)
 {
-    const uint32_t lane = lane_id();
     const uint32_t nwd = (m + 7) / 8 + 1;
     uint32_t *dst = reinterpret_cast<uint32_t *>(z.rd);
-    for (uint32_t w = lane; w < nwd; w += 64) {
+    for (uint32_t w = tid; w < nwd; w += T) {
         uint32_t c[9];
 #pragma unroll
         for (uint32_t b = 0; b < 9; ++b) {
@@ -314,6 +313,11 @@ __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
             x |= (c[2 * k] | c[2 * k + 1] << 2 | c[2 * k + 1] << 4 | c[2 * k + 2] << 6) << (8 * k);
         dst[w] = x;
     }
+}
+
+__device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
+{
+    stage_read(z, src, m, lane_id(), 64);
     wsync();
 }
 
@@ -2265,6 +2269,16 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     z.R = R2;
     z.cur = b;
     __syncthreads();
+#ifndef CCSX_STAGE_W0
+    // read k + 1 for the next DP, staged by all three waves (the helpers are
+    // idle until the DP's job barrier, which also publishes the writes);
+    // run_poa skips its own staging under the same condition
+    if (k + 1 < z.d.n) {
+        const uint32_t m1 = uni(P<uint32_t>(z, z.L.rdlen)[k + 1]);
+        if (m1 != 0 && m1 <= z.rdcap && m1 <= z.d.lcap)
+            stage_read(z, z.seq + uni(P<uint32_t>(z, z.L.rdoff)[k + 1]), m1, tid, T);
+    }
+#endif
 }
 
 // ----------------------------------------------------------------------------
@@ -2362,17 +2376,25 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
     z.E = 0;
     z.cur = 0;
     if (lane_id() == 0) G_poff(z, 0)[0] = 0;
+    bool staged = false;  // read k was staged by the previous merge (all waves)
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t m = uni(rdlen[k]);
         if (lane_id() == 0) rfirst[k] = rlast[k] = kNone;
         wsync();
-        if (m == 0) continue;
+        if (m == 0) {
+            staged = false;
+            continue;
+        }
         if (m > z.rdcap || m > z.d.lcap) {
             z.status = kErrReadLen;
             return 0;
         }
         unsigned long long t0 = stamp();
+#ifndef CCSX_STAGE_W0
+        if (!staged || zseq != z.seq) load_read(z, zseq + uni(rdoff[k]), m);
+#else
         load_read(z, zseq + uni(rdoff[k]), m);
+#endif
         unsigned long long t1 = stamp();
         z.pf[kPfLoad] += t1 - t0;
         if (z.R) {
@@ -2395,6 +2417,7 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             else merge<false>(z, k, m, threadIdx.x);
         }
         if (z.status) return 0;
+        staged = k + 1 < z.d.n;  // (the merge staged read k + 1 under run_poa's own checks)
         z.pf[kPfMerge] += stamp() - t1;
     }
     unsigned long long t3 = stamp();
