@@ -188,6 +188,8 @@ def main():
     ap.add_argument("--nzmw", type=int, default=0, help="override ZMWs per GPU (testing only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-zmws", type=int, default=16384, help="ZMWs per GPU of the end-to-end line (0: skip)")
+    ap.add_argument("--kcfg", type=int, default=-1, help="force a kernel configuration (0 latency, 1 occupancy, "
+                                                         "2 throughput; -1: by slice size)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.nzmw:
@@ -215,6 +217,8 @@ def main():
     sharing = (local_world + ndev - 1) // ndev
     if sharing > 1:
         eng.set_mem_share(sharing)
+    if args.kcfg >= 0:
+        eng.set_kernel_cfg(args.kcfg)
     eng.stage(zs)
     for _ in range(args.warmup):
         eng.launch(cfg["mode"])
@@ -270,7 +274,7 @@ def main():
                          "frac_vs_packed_int16": round(achieved / (2 * VALU_PEAK_TOPS), 5),
                          "traffic": load_traffic(args.config),
                          "kernel": "ccsx_zmw_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                         "ops_per_cell": OPS_PER_CELL},
+                         "ops_per_cell": OPS_PER_CELL, "kernel_cfg": eng.kernel_cfg()},
             "step_ms": [round(k, 3) for k in kernel_ms],
         }
         if sharing > 1:

@@ -30,9 +30,13 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 
 ARCH = os.environ.get("CCSX_OFFLOAD_ARCH", "gfx950")
 # the kernel configurations (ccsx_layout.h KernelCfg): latency (8-row DP
-# blocks, 32-row ring) and occupancy (4-row blocks, 24-row ring)
-KCFGS = [("lat", ["-DCCSX_KCFG=lat", "-DCCSX_LAUNCH=ccsx_launch_zmw_lat", "-DCCSX_RINGA=32", "-DCCSX_BLK=8"]),
-         ("occ", ["-DCCSX_KCFG=occ", "-DCCSX_LAUNCH=ccsx_launch_zmw_occ", "-DCCSX_RINGA=24", "-DCCSX_BLK=4"])]
+# blocks, 32-row ring), occupancy (4-row blocks, 24-row ring) and throughput
+# (two-wave workgroups)
+KCFGS = [(n, [f"-DCCSX_KCFG={n}", f"-DCCSX_LAUNCH=ccsx_launch_zmw_{n}", f"-DCCSX_INFO=ccsx_kcfg_info_{n}"] + d)
+         for n, d in [("lat", ["-DCCSX_RINGA=32", "-DCCSX_BLK=8"]),
+                      ("occ", ["-DCCSX_RINGA=24", "-DCCSX_BLK=4"]),
+                      # two-wave workgroups, a 16-row ring read back 8 rows
+                      ("tput", ["-DCCSX_RINGA=16", "-DCCSX_BLK=4", "-DCCSX_RING=8", "-DCCSX_HELPERS=1"])]]
 
 
 def _hipcc() -> str:

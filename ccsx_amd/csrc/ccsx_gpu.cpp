@@ -19,9 +19,42 @@
 
 #include "ccsx_layout.h"
 
-// the two kernel configurations (ccsx_layout.h KernelCfg), one object each
+// the kernel configurations (ccsx_layout.h KernelCfg), one object each: the
+// launcher and the configuration's own LDS / thread figures
 extern "C" hipError_t ccsx_launch_zmw_lat(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" hipError_t ccsx_launch_zmw_occ(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+extern "C" hipError_t ccsx_launch_zmw_tput(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+extern "C" void ccsx_kcfg_info_lat(ccsx::KCfgInfo *o);
+extern "C" void ccsx_kcfg_info_occ(ccsx::KCfgInfo *o);
+extern "C" void ccsx_kcfg_info_tput(ccsx::KCfgInfo *o);
+
+namespace {
+typedef hipError_t (*LaunchFn)(const ccsx::KArgs *, uint32_t, hipStream_t);
+constexpr LaunchFn kLaunch[ccsx::kCfgCount] = {ccsx_launch_zmw_lat, ccsx_launch_zmw_occ, ccsx_launch_zmw_tput};
+
+ccsx::KCfgInfo kcfg_info(int cfg)
+{
+    ccsx::KCfgInfo o{};
+    if (cfg == ccsx::kCfgLatency) ccsx_kcfg_info_lat(&o);
+    else if (cfg == ccsx::kCfgOccupancy) ccsx_kcfg_info_occ(&o);
+    else ccsx_kcfg_info_tput(&o);
+    return o;
+}
+
+// LDS bytes of a configuration's workgroup with `extra` words of read
+// buffer and cursors
+uint32_t kcfg_lds(int cfg, uint32_t extra) { return (kcfg_info(cfg).lds_fixed_words + extra) * 4u; }
+
+// workgroups per CU: 16 waves per CU (128 VGPRs, 4 waves per SIMD) and
+// 160 KiB of LDS
+uint32_t kcfg_wg_per_cu(int cfg, uint32_t extra)
+{
+    const ccsx::KCfgInfo i = kcfg_info(cfg);
+    const uint32_t by_waves = 16u / (i.threads / 64u);
+    const uint32_t by_lds = (160u * 1024u) / kcfg_lds(cfg, extra);
+    return std::min(by_waves, by_lds);
+}
+}  // namespace
 
 namespace {
 
@@ -317,13 +350,11 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
         c->lds_nmax = std::max<uint32_t>(nmax, 1);
     }
     // kernel configuration: the latency one if it keeps the whole slice
-    // resident (VGPRs: 16 waves per CU = 5 three-wave workgroups; LDS:
-    // 160 KiB), else the occupancy one (ccsx_layout.h KernelCfg)
+    // resident, else the occupancy one (ccsx_layout.h KernelCfg)
     {
-        const uint32_t lds_lat = uint32_t((ccsx::lds_fixed_words(ccsx::kCfgRingA[ccsx::kCfgLatency]) +
-                                           c->lds_read_words + c->lds_nmax) * 4);
-        const uint32_t wg = std::min<uint32_t>(5u, (160u * 1024u) / lds_lat);
-        c->cfg = c->cfg_force >= 0 ? c->cfg_force : (nz <= (size_t)c->ncu * wg ? ccsx::kCfgLatency : ccsx::kCfgOccupancy);
+        const uint32_t extra = c->lds_read_words + c->lds_nmax;
+        const size_t res_lat = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgLatency, extra);
+        c->cfg = c->cfg_force >= 0 ? c->cfg_force : (nz <= res_lat ? ccsx::kCfgLatency : ccsx::kCfgOccupancy);
     }
     size_t freeb = 0, totb = 0;
     const auto ti = std::chrono::steady_clock::now();
@@ -422,14 +453,13 @@ int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
         HIPCHK(c, c->d_prof.reserve(c->nz * ccsx::kProfSlots * 8));
         a.prof = c->d_prof.as<unsigned long long>();
     }
-    const uint32_t lds = uint32_t((ccsx::lds_fixed_words(ccsx::kCfgRingA[c->cfg]) + c->lds_read_words + c->lds_nmax) * 4);
+    const uint32_t lds = kcfg_lds(c->cfg, c->lds_read_words + c->lds_nmax);
     if (lds > 160 * 1024) {
         c->err = "reads too long for the LDS read buffer";
         return -1;
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, c->cfg == ccsx::kCfgLatency ? ccsx_launch_zmw_lat(&a, lds, c->stream)
-                                           : ccsx_launch_zmw_occ(&a, lds, c->stream));
+    HIPCHK(c, kLaunch[c->cfg](&a, lds, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     HIPCHK(c, hipEventSynchronize(c->ev1));
     float ms = 0.f;
@@ -623,7 +653,7 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *c, uint32_t rows)
 
 int ccsx_gpu_set_kernel_cfg(ccsx_ctx *c, int cfg)
 {
-    if (!c || cfg < -1 || cfg > 1) return -1;
+    if (!c || cfg < -1 || cfg >= ccsx::kCfgCount) return -1;
     c->cfg_force = cfg;
     return 0;
 }

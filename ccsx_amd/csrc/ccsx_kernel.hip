@@ -1,18 +1,24 @@
 // ccsx_kernel.hip -- MI355X (gfx950) consensus hot path of ccsx.
 //
-// One 64-lane wavefront owns one ZMW for the whole of ccs_for2 (main.c:510-647,
-// shredded mode) or ccs_for (main.c:455-508, -P): the window loop, every
-// bspoa call (beg/push/end/tidy_msa, SPEC.md §2-§6), the breakpoint scan and
-// the CCS emission all run on the device.  The host only runs ccs_prepare and
-// hands over strand-normalised segments.
+// One workgroup of three 64-lane waves owns one ZMW for the whole of ccs_for2
+// (main.c:510-647, shredded mode) or ccs_for (main.c:455-508, -P): the window
+// loop, every bspoa call (beg/push/end/tidy_msa, SPEC.md §2-§6), the
+// breakpoint scan and the CCS emission all run on the device.  The host only
+// runs ccs_prepare and hands over strand-normalised segments.
 //
-// Per DP row (one graph node, W = 128 read positions) each lane owns two
-// adjacent cells.  The in-row insertion recurrence is an exclusive prefix max
-// done with DPP row_shr / row_bcast (no LDS); the last kRing rows live in an
-// LDS ring in an even/odd split layout (conflict-free ds_read_b32 for any
-// band shift); rows needed further back are spilled to HBM.  Traceback codes
-// (4 bits/cell, plus predecessor slots for multi-predecessor nodes) stream to
-// HBM, coalesced, 64 B per row.
+// DP (SPEC.md §3): wave 0 runs the row recurrence -- per graph row W = 128
+// read positions, two adjacent cells per lane, band placement from the
+// predecessor's row maximum, the in-row insertion prefix max and the row-max
+// key as DPP max-scans -- and writes each row's H and D to an LDS ring of
+// kRingA rows, padded by 4 words of -inf per side so any band shift in
+// [-3, 4] is three immediate-offset reads.  Rows needed more than kRing rows
+// later are spilled to HBM.  Helper waves 1 and 2 follow one lockstep block
+// of kBlkAB rows behind, recompute each cell's decision bits from the ring
+// and store 16-bit cell records (code | D-ext | I-ext | M tag | D tag) to
+// HBM, 256 B per row, rotated per row for the traceback's LDS banks.
+// Traceback (SPEC.md §4) walks those records on wave 0 from 32-row blocks
+// LDS-DMA'd double-buffered; merge (§5) and the column counts (§6) run on all
+// three waves.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,6 +32,9 @@
 #endif
 #ifndef CCSX_LAUNCH
 #define CCSX_LAUNCH ccsx_launch_zmw_lat
+#endif
+#ifndef CCSX_INFO
+#define CCSX_INFO ccsx_kcfg_info_lat
 #endif
 
 namespace ccsx {
@@ -52,14 +61,14 @@ __device__ __forceinline__ int dpp(int old, int v)
 // step is max(v, dpp(INT_MIN, v)): with the max's identity as the DPP mov's
 // old value the compiler folds the mov into one v_max_i32_dpp and, unlike an
 // asm block, fills the VALU-write -> DPP-read wait states with independent
-// work of the row instead of s_nop (CCSX_ASM_SCAN: the hand-written form).
+// work of the row instead of s_nop (a hand-written asm
+// scan with s_nop measured slower).
 template <int CTRL, int RM = 0xF>
 __device__ __forceinline__ int dpp_max(int v)
 {
     return max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, CTRL, RM, 0xF, false));
 }
 
-#ifndef CCSX_ASM_SCAN
 __device__ __forceinline__ int wave_incl_max(int v)
 {
     v = dpp_max<0x111>(v);
@@ -76,58 +85,6 @@ __device__ __forceinline__ void wave_incl_max2(int &a, int &b)
     a = wave_incl_max(a);
     b = wave_incl_max(b);
 }
-#else
-// (hand-written form) inclusive max-scan: six in-place DPP max ops (a lane
-// whose DPP source is out of range, or whose row is masked, is not written,
-// i.e. keeps its own value).  Hand-written because hipcc does not fold the
-// DPP movs into the max; the s_nop 1 cover the VALU-write -> DPP-read hazard.
-__device__ __forceinline__ int wave_incl_max(int v)
-{
-    asm("s_nop 1\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-        "s_nop 1"
-        : "+v"(v));
-    return v;
-}
-
-// two independent inclusive max-scans, interleaved so each DPP op's hazard
-// wait is covered by the other chain's op (one s_nop 0 per pair instead of
-// two s_nop 1)
-__device__ __forceinline__ void wave_incl_max2(int &a, int &b)
-{
-    asm("s_nop 1\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_max_i32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 0\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_max_i32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 0\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_max_i32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 0\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_max_i32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 0\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-        "v_max_i32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-        "s_nop 0\n\t"
-        "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-        "v_max_i32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-        "s_nop 1"
-        : "+v"(a), "+v"(b));
-}
-
-#endif
 
 __device__ __forceinline__ int wave_incl_sum(int v)
 {
@@ -168,15 +125,6 @@ __device__ __forceinline__ int writelane(int v, int x, int l)
     return v;
 }
 
-#ifdef CCSX_WL_NV
-__device__ __forceinline__ int writelane_nv(int v, int x, int l)
-{
-    asm("v_writelane_b32 %0, %1, %2"
-        : "+v"(v)
-        : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(__builtin_amdgcn_readfirstlane(l)));
-    return v;
-}
-#endif
 
 __device__ __forceinline__ int wave_max(int v) { return __builtin_amdgcn_readlane(wave_incl_max(v), 63); }
 
@@ -210,7 +158,7 @@ struct Z {
     ZLayout L;
     uint8_t *ws;
     const uint8_t *seq;
-    int32_t *lds;        // ring: kRing * 256 ints
+    int32_t *lds;        // workgroup LDS: DP ring (kRingA rows x kRowW words), offsets, job, read
     uint8_t *rd;         // read as nibble pairs: byte b = pair(2b) | pair(2b+1) << 4, pair(j) = code(j) | code(j+1) << 2
     uint32_t *pos;       // shredding cursors
     uint32_t rdcap;      // bases that fit in rd
@@ -328,7 +276,6 @@ constexpr int kLdsOffRing = kLdsDiag + 32;               // 64: band offset of D
 constexpr int kLdsJob = kLdsOffRing + 64;                // 16: DP job / results
 constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
-static_assert(kLdsFixed == kLdsFixedWords, "host and device LDS layouts disagree");
 
 // per lane: row r0+lane's info and first four predecessors
 struct RowPre {
@@ -384,11 +331,7 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
 // 32-row traceback block, so the traceback's window fill -- 32 lanes reading
 // the same column of 32 consecutive rows -- spreads over the LDS banks instead
 // of hitting one (a 256 B pitch is a multiple of the 32-bank width).
-#ifdef CCSX_NO_ROT
-__device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return 0u * r; }  // (diagnostic variant)
-#else
 __device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; }
-#endif
 
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
@@ -396,7 +339,13 @@ constexpr int32_t kNegH = kNeg - kO - kE;
 #define CCSX_BLK 8
 #endif
 constexpr int kBlkAB = CCSX_BLK;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2, ...
-constexpr int kHelpers = 2;
+// helper waves per workgroup: 2 (latency / occupancy configurations) or 1
+// (throughput configuration: two-wave workgroups, twice the resident ZMWs)
+#ifndef CCSX_HELPERS
+#define CCSX_HELPERS 2
+#endif
+constexpr int kHelpers = CCSX_HELPERS;
+static_assert(kHelpers == 1 || kHelpers == 2, "one or two helper waves");
 constexpr int kBlockThreads = 64 * (1 + kHelpers);
 static_assert(kBlkAB % kHelpers == 0, "each helper takes the same number of rows per block");
 // issue priorities (s_setprio): wave 0 always, helpers during merge; helpers
@@ -814,26 +763,13 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         }
         const int32_t key = __builtin_amdgcn_readlane(rk, 63);
         // ring row, meta window
-#ifdef CCSX_RING_INC
-        (void)ring;
-        int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + S.ring + kHc + c.L2);
-#else
         int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
-#endif
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
         // (inline asm measured 0.6 % faster than the compiler's writelane
         // intrinsic here: it keeps vOff / vKey out of the scheduler's way)
-#if defined(CCSX_WL_BUILTIN)
-        S.vOff = __builtin_amdgcn_writelane(off, li, S.vOff);
-        S.vKey = __builtin_amdgcn_writelane(key, li, S.vKey);
-#elif defined(CCSX_WL_NV)
-        S.vOff = writelane_nv(S.vOff, off, li);
-        S.vKey = writelane_nv(S.vKey, key, li);
-#else
         S.vOff = writelane(S.vOff, off, li);
         S.vKey = writelane(S.vKey, key, li);
-#endif
         if (cold && (info & kInfoSpill)) {
             // a successor lies beyond the ring: keep this row in HBM
             const uint32_t sl = S.nspill++;
@@ -850,9 +786,6 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
         S.pOff = off;
         S.pArg = off + 127 - (key & 127);
-#ifdef CCSX_RING_INC
-        S.ring = S.ring + kRowW == (uint32_t)(kRingA * kRowW) ? 0u : S.ring + kRowW;
-#endif
 #ifdef CCSX_DP_STAMPS
         if (!cold && ckind != 6) {
             ROW_STAMP(ts2);
@@ -888,17 +821,6 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         // of -inf (SPEC.md §3.2 src(0) = 0): it rides in as the DPP's old
         // value, max(0, src) = 0, so the tail needs no lane test.
         const uint32_t qp = S.qn >> (4u * (uint32_t)(coff - pb));  // coff - pb in [0, 2]
-#ifdef CCSX_FAST_SELECT
-        const bool s1 = sh != 0;
-        const int32_t hL = wave_shr1(coff == 0 ? 0 : kNegH, S.H1), hR = wave_shl1(kNegH, S.H0),
-                      dR = wave_shl1(kNeg, S.D0);
-        const int32_t Mh0 = s1 ? S.H0 : hL;
-        const int32_t Mh1 = s1 ? S.H1 : S.H0;
-        const int32_t hC = s1 ? hR : S.H1, dB = s1 ? S.D1 : S.D0, dC = s1 ? dR : S.D1;
-        const int32_t Dv0 = max(Mh1 + (kO + kE), dB + kE);
-        const int32_t Dv1 = max(hC + (kO + kE), dC + kE);
-        tail(coff, qp, Mh0, Mh1, Dv0, Dv1, false);
-#else
         // band move 0 or 1 as a scalar branch: each side shifts only what it
         // needs (no selects)
         if (sh == 0) {
@@ -912,7 +834,6 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
             const int32_t Dv1 = max(hR + (kO + kE), dR + kE);
             tail(coff, qp, S.H0, S.H1, Dv0, Dv1, false);
         }
-#endif
     } else {
         int32_t off, Mh0, Mh1, Dv0, Dv1;
         int kind;
@@ -1025,29 +946,12 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
         // D > H + O + E (D = max(H + O + E, D' + E))
         const int32_t *row = z.lds + kLdsRing + (p0 % kRingA) * kRowW;
         const int32_t *b = row + (kHc - 1) + c.L2 + sh;  // cell 2l + sh - 1
-#ifndef CCSX_HELPER_B64
         // three ds_read_b32 at a 2-word lane stride: a 2-way bank conflict
-        // each.  (Variant CCSX_HELPER_B64 -- one aligned ds_read_b64 per lane,
-        // the third cell by DPP -- cut SQ_LDS_BANK_CONFLICT 1.54e9 -> 1.12e9
+        // each.  (A variant with one aligned ds_read_b64 per lane and
+        // the third cell by DPP cut SQ_LDS_BANK_CONFLICT 1.54e9 -> 1.12e9
         // per launch but ran 1.5 % slower: the parity branch and edge-lane
         // read cost the near-critical helpers more; tools/gpu_lds_ab.sh r02y)
         const int32_t hA = b[0], hB = b[1], hC = b[2];
-#else
-        // one 8-byte-aligned pair per lane (consecutive 8 B across the lanes:
-        // no LDS bank conflict) and the third cell from the neighbour lane by
-        // DPP.  The edge lane's cell (lane 63: 127 + sh, lane 0: sh - 1) is
-        // the pad -inf for the usual shifts 0 / 1, one broadcast read else.
-        int32_t hA, hB, hC;
-        if (sh & 1) {  // cell 2l + sh - 1 even: (hA, hB) aligned
-            const int2 v = *reinterpret_cast<const int2 *>(b);
-            const int32_t e = sh < 0 ? row[kHc + kW - 1 + sh] : kNegH;
-            hA = v.x, hB = v.y, hC = wave_shl1(e, v.x);
-        } else {  // (hB, hC) aligned
-            const int2 v = *reinterpret_cast<const int2 *>(b + 1);
-            const int32_t e = sh > 0 ? row[kHc + sh - 1] : kNegH;
-            hB = v.x, hC = v.y, hA = wave_shr1(e, v.y);
-        }
-#endif
         A.Mh0 = hA, A.Mh1 = hB;
         A.ms0 = A.ms1 = A.ds0 = A.ds1 = r - p0;
         A.dx0 = A.Dv0 > hB + (kO + kE) ? 4u : 0u;
@@ -1159,13 +1063,20 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
         DP_STAMP(kPfAwait);
     }
     // the two helpers' candidates cover disjoint rows: max score, then min row
-    const int32_t b0 = uni(job->res[0].best), b1 = uni(job->res[1].best);
-    const uint32_t r0 = uni(job->res[0].er), r1 = uni(job->res[1].er);
-    const bool second = b1 > b0 || (b1 == b0 && r1 < r0);
-    er_out = second ? r1 : r0;
-    ej_out = second ? uni(job->res[1].ej) : uni(job->res[0].ej);
-    const int32_t s0 = uni(job->res[0].status), s1 = uni(job->res[1].status);
-    const int32_t bst = s0 ? s0 : s1;
+    int32_t bst;
+    if (kHelpers == 1) {
+        er_out = uni(job->res[0].er);
+        ej_out = uni(job->res[0].ej);
+        bst = uni(job->res[0].status);
+    } else {
+        const int32_t b0 = uni(job->res[0].best), b1 = uni(job->res[1].best);
+        const uint32_t r0 = uni(job->res[0].er), r1 = uni(job->res[1].er);
+        const bool second = b1 > b0 || (b1 == b0 && r1 < r0);
+        er_out = second ? r1 : r0;
+        ej_out = second ? uni(job->res[1].ej) : uni(job->res[0].ej);
+        const int32_t s0 = uni(job->res[0].status), s1 = uni(job->res[1].status);
+        bst = s0 ? s0 : s1;
+    }
     if (bst && !z.status) z.status = bst;
     z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
 }
@@ -1254,7 +1165,7 @@ __device__ __forceinline__ void dp_helper_exit(Z &z)
     // the helper waves hand over their diagnostic counters
     __syncthreads();
     const volatile unsigned long long *pf1 = reinterpret_cast<const volatile unsigned long long *>(z.lds + kLdsDiag);
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kHelpers; ++h) {
         z.pf[kPfBbusy] += pf1[8 * h + 0];
         z.pf[kPfBwait] += pf1[8 * h + 1];
         z.pf[kPfSpare2] += pf1[8 * h + 2];
@@ -1329,18 +1240,9 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
     const uint32_t lane = lane_id();
     const uint8_t *src = z.ws + z.L.codes + (size_t)bi * kTbRows * 256 + lane * 16u;
     int32_t *dst = z.lds + buf * kTbBufWords;
-#ifdef CCSX_TB_DMA_B32
-    // (diagnostic variant: 4 B per lane, one row per instruction)
-    const uint8_t *s4 = z.ws + z.L.codes + (size_t)bi * kTbRows * 256 + lane * 4u;
-#pragma unroll
-    for (int k = 0; k < 32; ++k)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(s4 + k * 256), dst + k * 64, 4, 0, 0);
-    (void)src;
-#else
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(src + k * 1024), dst + k * 256, 16, 0, 0);
-#endif
     const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + bi * kTbRows + lane;
     __builtin_amdgcn_global_load_lds(ms, z.lds + 2 * kTbBufWords + buf * 64, 4, 0, 0);
 }
@@ -1358,31 +1260,20 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
 // caller swaps in the next window).  The walk keeps li = r - base as its own
 // variable and leaves high-half records in place (their tag and code are read
 // at bit 20 / 16), so the dependent chain of a step is s_bfe -> s_sub ->
-// v_readlane; a step is 11 instructions.  (CCSX_TB_W64: the previous form,
-// one 64-lane window, li recomputed and the half shifted down per step, 14.)
+// v_readlane; a step is 11 instructions (a 64-lane window with li recomputed
+// and the half shifted down per step took 14).
 // Hand-written: compiled, the multi-exit unrolled loop became a flag-driven
 // state machine of ~35 scalar instructions per step.  (Handling D / I steps
 // inside the window as well measured no faster: tools/gpu_ab.sh r02u.)
-#ifndef CCSX_TB_W64
 // leave the window walk when the predecessor row lies below the block
-// (tag > li; CCSX_TB_GE: also when it is the block's first row)
-#ifdef CCSX_TB_GE
-#define TBW_LEAVE "s_cmp_ge_u32 %[t], %[li]\n\t"
-#else
+// (tag > li: a step may land on the block's first row)
 #define TBW_LEAVE "s_cmp_gt_u32 %[t], %[li]\n\t"
-#endif
 __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t wa, uint32_t wb, uint32_t &r,
                                             int32_t &j, uint32_t &rec, uint32_t &vev, uint32_t &st)
 {
     uint32_t t, li, c, jh, m0v;
     // the asm's scalar operands must live in SGPRs
     r = uni(r), j = uni(j), rec = uni(rec), k = uni(k), base = uni(base);
-#ifdef CCSX_TBW_JSUB
-#define TBW_M0 "s_and_b32 %[m0], %[j], 63\n\t"
-#define TBW_J "s_sub_u32 %[j], %[j], 1\n\t"
-#define TBW_ENTRY ""
-#define TBW_EXIT ""
-#else
 // m0 = j & 63 is kept by the walk (the window's columns never cross a
 // 64-base chunk: jw = 0 mod 4 and the last column leaves on a completed
 // chunk), j rebuilt from it at the exits
@@ -1390,7 +1281,6 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
 #define TBW_J "s_sub_u32 %[m0], %[m0], 1\n\t"
 #define TBW_ENTRY "s_and_b32 %[m0], %[j], 63\n\ts_andn2_b32 %[jh], %[j], 63\n\t"
 #define TBW_EXIT "s_or_b32 %[j], %[jh], %[m0]\n\t"
-#endif
 #define TBW_HEAD(BFE, SLOW)                              \
     TBW_M0                                               \
     "v_writelane_b32 %[vev], %[r], %[m0]\n\t"            \
@@ -1456,62 +1346,6 @@ __device__ __forceinline__ uint32_t tb_wb(uint32_t win)
 {
     return (uint32_t)__builtin_amdgcn_permlane32_swap(win, win, false, false)[1];
 }
-#else
-__device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t win, uint32_t &r, int32_t &j,
-                                            uint32_t &rec, uint32_t &vev, uint32_t &st)
-{
-    uint32_t t, li, m0v;
-    // the asm's scalar operands must live in SGPRs
-    r = uni(r), j = uni(j), rec = uni(rec), k = uni(k), base = uni(base);
-#define TBW_HEAD                                         \
-    "s_and_b32 %[m0], %[j], 63\n\t"                      \
-    "v_writelane_b32 %[vev], %[r], %[m0]\n\t"            \
-    "s_bfe_u32 %[t], %[rec], 0x60004\n\t"                \
-    "s_sub_u32 %[li], %[r], %[base]\n\t"                 \
-    "s_cmp_ge_u32 %[t], %[li]\n\t"                       \
-    "s_cbranch_scc1 .Ltbw_slow%=\n\t"
-#define TBW_MOVE                                         \
-    "s_sub_u32 %[j], %[j], 1\n\t"                        \
-    "s_sub_u32 %[r], %[r], %[t]\n\t"
-#define TBW_NEXT(LANEOR, HALF)                           \
-    "s_sub_u32 %[li], %[r], %[base]\n\t" LANEOR          \
-    "v_readlane_b32 %[rec], %[win], %[li]\n\t" HALF      \
-    "s_and_b32 %[t], %[rec], 3\n\t"                      \
-    "s_cbranch_scc1 .Ltbw_out%=\n\t"
-    asm volatile(
-        "s_cmp_eq_u32 %[k], 0\n\t"
-        "s_cbranch_scc1 .Ltbw_0%=\n\t"
-        "s_cmp_eq_u32 %[k], 1\n\t"
-        "s_cbranch_scc1 .Ltbw_1%=\n\t"
-        "s_cmp_eq_u32 %[k], 2\n\t"
-        "s_cbranch_scc1 .Ltbw_2%=\n\t"
-        "s_branch .Ltbw_3%=\n"
-        ".Ltbw_0%=:\n\t" TBW_HEAD TBW_MOVE TBW_NEXT("", "s_lshr_b32 %[rec], %[rec], 16\n\t")
-        ".Ltbw_1%=:\n\t" TBW_HEAD TBW_MOVE TBW_NEXT("s_or_b32 %[li], %[li], 32\n\t", "s_and_b32 %[rec], %[rec], 0xffff\n\t")
-        ".Ltbw_2%=:\n\t" TBW_HEAD TBW_MOVE TBW_NEXT("s_or_b32 %[li], %[li], 32\n\t", "s_lshr_b32 %[rec], %[rec], 16\n\t")
-        ".Ltbw_3%=:\n\t" TBW_HEAD
-        "s_cmp_eq_u32 %[m0], 0\n\t"
-        "s_cbranch_scc1 .Ltbw_slow%=\n\t" TBW_MOVE
-        "s_mov_b32 %[st], 0\n\t"
-        "s_branch .Ltbw_end%=\n"
-        ".Ltbw_slow%=:\n\t"
-        "s_mov_b32 %[st], 1\n\t"
-        "s_branch .Ltbw_end%=\n"
-        ".Ltbw_out%=:\n\t"
-        "s_mov_b32 %[st], 2\n"
-        ".Ltbw_end%=:"
-        : [r] "+s"(r), [j] "+s"(j), [rec] "+s"(rec), [vev] "+v"(vev), [st] "=s"(st), [t] "=&s"(t), [li] "=&s"(li),
-          [m0] "=&{m0}"(m0v)
-        : [k] "s"(k), [base] "s"(base), [win] "v"(win)
-        : "scc");
-    // (the divergence analysis takes inline-asm results as divergent: without
-    // these, everything downstream of r / j would go to VGPRs and exec masks)
-    r = uni(r), j = uni(j), rec = uni(rec), st = uni(st);
-#undef TBW_HEAD
-#undef TBW_MOVE
-#undef TBW_NEXT
-}
-#endif
 
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
@@ -1539,12 +1373,8 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         voff = mt & 0x7FFFFFFFu;
         vrot = (tb_rot(lane) - 2u * voff) & 255u;
         farm = (uint32_t)ballot((mt >> 31) != 0u);
-#ifdef CCSX_TB_BPERM
-        vrot32 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & 31u) * 4u), (int)vrot) - ((lane >> 5) * 4u);
-#else
         // lanes 32-63 take lane l - 32's rotation (v_permlane32_swap: no LDS)
         vrot32 = (uint32_t)__builtin_amdgcn_permlane32_swap(vrot, vrot, false, false)[0] - ((lane >> 5) * 4u);
-#endif
         rowb32 = (buf * 32u + (lane & 31u)) << 8;
         jw = INT32_MIN / 2;
         jwn = INT32_MAX;
@@ -1607,13 +1437,6 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         t_prev += ts1 - ts0;
 #endif
     };
-    // the record of cell (r, j); r must lie in the staged block
-    auto rec_at = [&]() -> uint32_t {
-        const uint32_t li = r - base;
-        const uint32_t a = ((buf * 32u + li) << 8) |
-                           (((uint32_t)__builtin_amdgcn_readlane((int)vrot, (int)li) + 2u * (uint32_t)j) & 255u);
-        return uni((uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + a));
-    };
     // the record window of columns [jwv - 4, jwv) of the staged block (layout
     // at vrot32 above); the compiler's lgkmcnt wait lands at the first use
     auto tb_win = [&](int32_t jwv) -> uint32_t {
@@ -1627,25 +1450,18 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     // (one LDS round trip, which the window steps then reuse); r must lie in
     // the staged block
     auto rec_win = [&]() -> uint32_t {
-#ifndef CCSX_TB_DI_LDS
         uint32_t kk = (uint32_t)(jw - 1 - j);
         if (kk < 4u)
             return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
                     ((kk & 1u) * 16u)) & 0xFFFFu;
-#ifndef CCSX_TB_NO_WNX
         if (kk < 8u && jwn == jw)
             return ((uint32_t)__builtin_amdgcn_readlane((int)wnx, (int)((r - base) + ((kk & 2u) << 4))) >>
                     ((kk & 1u) * 16u)) & 0xFFFFu;
-#endif
-#ifndef CCSX_TB_REC_LDS
         jw = (j & ~3) + 4;
         win = tb_win(jw);
         kk = (uint32_t)(jw - 1 - j);
         return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
                 ((kk & 1u) * 16u)) & 0xFFFFu;
-#endif
-#endif
-        return rec_at();
     };
     auto cell = [&]() -> uint32_t {
         if (r < base) to_block();
@@ -1690,20 +1506,16 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
 #endif
         const uint32_t hc = rec & 3u;
         bool emitted = false;  // (r, j) MPRED, emitted by the window steps: its move is pending
-#if !defined(CCSX_TB_NOWIN) && !defined(CCSX_TB_WIN1)
         if (hc == HC_MPRED && farm == 0u) {
             // A block without far rows: plain steps through 4-column windows
             // aligned to jw = 0 mod 4 (tb_w4_steps), the next window read
             // from LDS while this one is walked.
             uint32_t k = (uint32_t)(jw - 1 - j);
             if (k >= 4u) {
-#ifndef CCSX_TB_NO_WNX
                 if (jwn == jw && k < 8u) {
                     win = wnx;  // j moved into the window below (already read)
                     jw -= 4;
-                } else
-#endif
-                {
+                } else {
                     jw = (j & ~3) + 4;
                     win = tb_win(jw);
                 }
@@ -1720,11 +1532,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             z.pf[kPfRowA] += 1;
 #endif
             for (;;) {
-#ifndef CCSX_TB_W64
                 tb_w4_steps(k, base, win, tb_wb(win), r, j, rec, vev, st);
-#else
-                tb_w4_steps(k, base, win, r, j, rec, vev, st);
-#endif
                 if (st) break;
                 win = wnx;
                 jw -= 4;
@@ -1745,7 +1553,6 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             if (st == 2) continue;  // a D / I / MSRC record at the new (r, j)
             emitted = true;
         }
-#endif
         if (hc == HC_MPRED) {  // state H
             if (!emitted) {
                 // plain steps while the next cell is in the block, the row not
@@ -1754,89 +1561,33 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                     emit((EV_ALN << 30) | r);
                     const uint32_t tag = (rec >> 4) & 63u;
                     const uint32_t li = r - base;
-#ifdef CCSX_TB_NOWIN
-                    const uint32_t slow = ((farm >> li) & 1u) | ((j & 63) == 0 ? 1u : 0u) | (tag >= li ? 1u : 0u) |
-                                          ((rec & 0x3F3u) == 0x10u ? 1u : 0u);
-#else
                     // sign-bit arithmetic keeps the test on the scalar unit (a
                     // compare of a bool lowers to VALU selects): far row, a chunk
                     // completes ((j & 63) == 0), or the predecessor leaves the block
-#ifdef CCSX_TB_GE
-                    const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag - 1u) >> 31)) & 1u;
-#else
                     const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag) >> 31)) & 1u;
-#endif
-#endif
                     if (slow) break;
                     --j;
                     r -= tag;
-#ifdef CCSX_TB_NOWIN
-                    rec = rec_at();
-#else
                     // r stays inside the block (tag < li): the next record comes
                     // from the window by one readlane; an LDS round trip only
                     // every fourth column
                     uint32_t k = (uint32_t)(jw - 1 - j);
                     if (k >= 4u) {
-#ifdef CCSX_TB_WIN1
-                        jw = j + 1;
-#else
                         jw = (j & ~3) + 4;  // aligned, as the unrolled loop above assumes
-#endif
                         win = tb_win(jw);
                         k = (uint32_t)(jw - 1 - j);
                     }
                     rec = ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((k & 2u) << 4))) >>
                            ((k & 1u) * 16u)) & 0xFFFFu;
-#endif
                     if ((rec & 3u) != HC_MPRED) break;
                 }
                 if ((rec & 3u) != HC_MPRED) continue;
-            }
-            bool probed = false;
-            // (CCSX_TB_PROBE: walk a run of tag-1 diagonal cells by one lane
-            // vector test here; with the windows it measured 0.3 % slower,
-            // A/B r02s9)
-#ifdef CCSX_TB_PROBE
-            if ((rec & 0x3F3u) == 0x10u && !((farm >> (r - base)) & 1u) && (j & 63) != 0 && r > base) {
-#else
-            if (false) {
-#endif
-                // diagonal run: lane i checks that cell (r-1-i, j-1-i) is MPRED to
-                // the row above it, inside this block and this event chunk; the
-                // run's events go into vev by one lane permutation
-                const int32_t i = (int32_t)lane;
-                const int32_t ri = (int32_t)(r - base) - 1 - i, ji = j - 1 - i;
-                const bool in = ri >= 0 && (ji & ~63) == chunk;
-                const uint32_t oi = (uint32_t)__builtin_amdgcn_ds_bpermute((in ? ri : 0) * 4, (int)voff);
-                const uint32_t ti = (uint32_t)ji - oi;
-                const bool inb = in && ti < (uint32_t)kW;
-                const uint32_t ab = ((buf * 32u + (uint32_t)ri) << 8) | ((2u * ti + tb_rot((uint32_t)ri)) & 255u);
-                const uint32_t rc = inb ? (uint32_t)*reinterpret_cast<const uint16_t *>(lds8 + ab) : 0u;
-                const bool ok = inb && !((farm >> (uint32_t)(in ? ri : 0)) & 1u) && (rc & 0x3F3u) == 0x10u;
-                const uint64_t bad = ~ballot(ok);
-                const uint32_t k = (uint32_t)__builtin_ctzll(bad);  // cells r-1 .. r-k continue the run (k < 64)
-                // base b = j - 1 - i gets ALN | (r - 1 - i): lane b & 63 reads lane (j - 1 - b) & 63
-                const uint32_t src = (uint32_t)(j - 1 - (int32_t)(chunk + (int32_t)lane)) & 63u;
-                const uint32_t val = (EV_ALN << 30) | (r - 1 - lane);
-                const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4u), (int)val);
-                const int32_t b = chunk + (int32_t)lane;
-                if (b <= j - 1 && b > j - 1 - (int32_t)k) vev = got;
-#ifdef CCSX_TB_COUNTING
-                z.pf[kPfSpare1] += k;
-                z.pf[kPfRowD] += 1;
-#endif
-                j -= (int32_t)k;
-                r -= k;
-                probed = true;
             }
             step_j();
             to_pred((rec >> 4) & 63u, j + 1, 0u);  // the MPRED cell is (r, j + 1)
             if (r < base) to_block();
             rec = rec_win();
-            if (probed) DP_STAMP(kPfTbProbe);
-            else DP_STAMP(kPfTbStep);
-            (void)probed;
+            DP_STAMP(kPfTbStep);
 #if defined(CCSX_TB_COUNT) && !defined(CCSX_DP_STAMPS)
             TB_MARK(kPfTbProbe);
 #endif
@@ -1955,11 +1706,7 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
 // round trips.  Larger graphs (-P) take the same steps through HBM.
 __device__ __forceinline__ bool merge_in_lds(uint32_t R)
 {
-#ifdef CCSX_NO_LM
-    return false && R;  // (diagnostic variant: merge through HBM only)
-#else
     return (R + 1) * 5u + 64u <= (uint32_t)(kRingA * kRowW * 4);
-#endif
 }
 
 template <bool LM>
@@ -2269,7 +2016,6 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     z.R = R2;
     z.cur = b;
     __syncthreads();
-#ifndef CCSX_STAGE_W0
     // read k + 1 for the next DP, staged by all three waves (the helpers are
     // idle until the DP's job barrier, which also publishes the writes);
     // run_poa skips its own staging under the same condition
@@ -2278,7 +2024,6 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
         if (m1 != 0 && m1 <= z.rdcap && m1 <= z.d.lcap)
             stage_read(z, z.seq + uni(P<uint32_t>(z, z.L.rdoff)[k + 1]), m1, tid, T);
     }
-#endif
 }
 
 // ----------------------------------------------------------------------------
@@ -2320,7 +2065,7 @@ __device__ __forceinline__ void columns_count(const Z &z, uint32_t n, uint32_t n
 
 // Column numbering and the reads' first / last columns on wave 0, then the
 // per-column counts on all three waves (job kJobColumns: the helpers join at
-// the two barriers after the job barrier; CCSX_COLS_W0: wave 0 alone)
+// the two barriers after the job barrier)
 __device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
 {
     const uint32_t lane = lane_id();
@@ -2330,11 +2075,9 @@ __device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
     uint32_t *colrow = P<uint32_t>(z, z.L.colrow);
     const uint32_t *rfirst = P<uint32_t>(z, z.L.rfirst), *rlast = P<uint32_t>(z, z.L.rlast);
     uint32_t *rfc = P<uint32_t>(z, z.L.rfc), *rlc = P<uint32_t>(z, z.L.rlc);
-#ifndef CCSX_COLS_W0
     volatile DpJob *job = dp_job(z);
     if (lane == 0) job->kind = kJobColumns, job->m = n, job->R = R, job->cur = (uint32_t)z.cur;
     __syncthreads();  // J: job posted
-#endif
     uint32_t carry = 0;
     for (uint32_t r0 = 0; r0 < R; r0 += 64) {
         const uint32_t r = r0 + lane;
@@ -2352,16 +2095,10 @@ __device__ __forceinline__ uint32_t call_columns(Z &z, uint32_t n)
         rfc[k] = rfirst[k] != kNone ? colof[rfirst[k]] : kNone;
         rlc[k] = rfirst[k] != kNone ? colof[rlast[k]] : 0u;
     }
-#ifndef CCSX_COLS_W0
     if (lane == 0) job->K = ncols;
     __syncthreads();  // columns numbered, ncols posted
     columns_count(z, n, ncols, threadIdx.x, kBlockThreads);
     __syncthreads();  // every column counted
-#else
-    wsync();
-    columns_count(z, n, ncols, lane, 64);
-    wsync();
-#endif
     return ncols;
 }
 
@@ -2390,11 +2127,7 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             return 0;
         }
         unsigned long long t0 = stamp();
-#ifndef CCSX_STAGE_W0
         if (!staged || zseq != z.seq) load_read(z, zseq + uni(rdoff[k]), m);
-#else
-        load_read(z, zseq + uni(rdoff[k]), m);
-#endif
         unsigned long long t1 = stamp();
         z.pf[kPfLoad] += t1 - t0;
         if (z.R) {
@@ -2664,10 +2397,21 @@ ccsx_zmw_kernel_hbm(KArgs a)
 }  // namespace CCSX_KCFG
 }  // namespace ccsx
 
-// lds_read_words == 0 selects the HBM-read instance (ccsx_gpu.cpp decides)
+// lds_read_words == 0 selects the HBM-read instance (ccsx_gpu.cpp decides);
+// lds_bytes = this configuration's fixed words (CCSX_INFO) + the read buffer
+extern "C" void CCSX_INFO(ccsx::KCfgInfo *o)
+{
+    namespace K = ccsx::CCSX_KCFG;
+    o->lds_fixed_words = (uint32_t)K::kLdsFixed;
+    o->threads = (uint32_t)K::kBlockThreads;
+    o->ring_rows = (uint32_t)ccsx::kRingA;
+    o->ring_back = (uint32_t)ccsx::kRing;
+}
+
 extern "C" hipError_t CCSX_LAUNCH(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s)
 {
     namespace K = ccsx::CCSX_KCFG;
+    if (lds_bytes < (uint32_t)K::kLdsFixed * 4u) return hipErrorInvalidValue;
     const void *f = a->lds_read_words ? reinterpret_cast<const void *>(&K::ccsx_zmw_kernel)
                                       : reinterpret_cast<const void *>(&K::ccsx_zmw_kernel_hbm);
     if (lds_bytes > 65536) {

@@ -18,7 +18,12 @@
 namespace ccsx {
 
 constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
-constexpr int kRing = 16;      // DP rows kept in LDS per wave
+// DP rows back whose H / D a row reads from the LDS ring (farther
+// predecessors: HBM spill records); per kernel configuration
+#ifndef CCSX_RING
+#define CCSX_RING 16
+#endif
+constexpr int kRing = CCSX_RING;
 constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H and D, each [4 pad | 128 | 4 pad]
 #ifndef CCSX_RINGA
 #define CCSX_RINGA 32
@@ -29,21 +34,26 @@ constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H a
 constexpr int kRingA = CCSX_RINGA;
 constexpr int kNeg = -(1 << 29);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-// fixed LDS words per workgroup: DP ring, helpers' diagnostic counters, band
-// offsets, job; the read and the shredding cursors follow (ccsx_kernel.hip)
-// fixed LDS words of a kernel configuration with a ring of `ringa` rows
-CCSX_HD constexpr int lds_fixed_words(int ringa) { return ringa * kRowW + 32 + 64 + 16; }
-constexpr int kLdsFixedWords = lds_fixed_words(kRingA);
 
-// The two LDS kernel configurations (ccsx_kernel.hip is compiled once per
+// The kernel configurations (ccsx_kernel.hip is compiled once per
 // configuration, ccsx_gpu.cpp picks one per slice):
-//  * latency: 8-row lockstep blocks and a 32-row ring -- the shortest
-//    per-ZMW chain, 4 workgroups per CU (config B: 1,000 ZMWs in one wave of
-//    workgroups);
-//  * occupancy: 4-row blocks and a 24-row ring -- 5 workgroups per CU, for
-//    slices larger than the latency configuration keeps resident.
-enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1 };
-constexpr int kCfgRingA[2] = {32, 24};
+//  * latency: three waves, 8-row lockstep blocks and a 32-row ring -- the
+//    shortest per-ZMW chain, 4 workgroups per CU (config B: 1,000 ZMWs in one
+//    wave of workgroups);
+//  * occupancy: three waves, 4-row blocks and a 24-row ring -- 5 workgroups
+//    per CU, for slices larger than the latency configuration keeps resident;
+//  * throughput: two waves (one helper), 4-row blocks, a 16-row ring of which
+//    the last 8 rows are read back -- up to 8 workgroups per CU, for slices of
+//    thousands of ZMWs, where resident ZMWs rather than per-ZMW latency bound
+//    the launch.
+// Each configuration's object reports its own LDS words and threads
+// (KCfgInfo), so the host never restates the build flags.
+enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1, kCfgThroughput = 2, kCfgCount = 3 };
+struct KCfgInfo {
+    uint32_t lds_fixed_words;  // LDS words before the read buffer
+    uint32_t threads;          // workgroup size
+    uint32_t ring_rows, ring_back;
+};
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch
 enum Status : int32_t {

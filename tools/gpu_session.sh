@@ -1,0 +1,75 @@
+#!/bin/bash
+# One GPU-box call made of named steps, each under its own time limit and
+# chained so the first failure ends the call (no GPU step after a fault).
+#
+#   gpurun --timeout 1200 -- bash tools/gpu_session.sh TAG STEP [STEP ...]
+#
+# Steps (output under gpurun_out/TAG/):
+#   tests              the -m gpu suite (python -u, per-test timeout)
+#   parity             tests/test_gpu_parity.py only
+#   bench              the default bench.py line (config B, 20 steps, e2e, cpu baseline)
+#   bench:CFG[:KCFG]   bench.py --config CFG (B|C|D|E|H), 3 steps, optional forced kernel cfg
+#   ab:CFG:KCFG,...    interleaved rounds of bench --config CFG over several kernel cfgs
+#   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
+#   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
+#   cli:N              CLI end to end on N config-E ZMWs streamed on stdin (tools/cli_e2e.py)
+# Environment: CCSX_LIB selects a library variant for the bench steps.
+set -o pipefail
+TAG=$1; shift
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$R" || exit 1
+
+bench_args() {  # CFG [KCFG]
+  local a="--config $1 --steps 3 --warmup 1 --no-cpu-baseline --e2e-zmws 0"
+  [ -n "$2" ] && a="$a --kcfg $2"
+  echo "$a"
+}
+
+step() {
+  local s=$1 name cfg k
+  IFS=: read -r name cfg k <<< "$s"
+  case $name in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gputest.log" 2>&1
+      local rc=$?; tail -3 "$OUT/gputest.log"; return $rc ;;
+    parity)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/parity.log" 2>&1
+      local rc=$?; tail -3 "$OUT/parity.log"; return $rc ;;
+    bench)
+      if [ -z "$cfg" ]; then
+        timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" && cat "$OUT/bench.json"
+        return $?
+      fi
+      local f="$OUT/bench_${cfg}${k:+_k$k}.json"
+      timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$k") > "$f" 2> "${f%.json}.err" &&
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['value'], 'ZMWs/s', d['gcups'], 'GCUPS', 'cfg', d['roofline'].get('kernel_cfg'))" "$f" ;;
+    ab)
+      local i kk f
+      for i in 1 2 3; do
+        for kk in ${k//,/ }; do
+          f="$OUT/ab_${cfg}_k${kk}_$i.json"
+          timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$kk") > "$f" 2> "${f%.json}.err" || return 1
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['gcups'], 'GCUPS')" "$f"
+        done
+      done ;;
+    kt)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_$cfg" -o kt -- \
+        python3 "$R/bench.py" --config "$cfg" --no-cpu-baseline --e2e-zmws 0 > "$OUT/kt_$cfg.json" 2> "$OUT/kt_$cfg.err") &&
+        echo "kt $cfg done" ;;
+    pmc)
+      timeout -k 10 900 bash "$R/tools/pmc_pass.sh" "$TAG/pmc_$cfg" --config "$cfg" > "$OUT/pmc_$cfg.log" 2>&1 && echo "pmc $cfg done" ;;
+    cli)
+      timeout -k 10 900 python -u tools/cli_e2e.py --n "$cfg" --out "$OUT" > "$OUT/cli_$cfg.log" 2>&1; local rc=$?
+      tail -5 "$OUT/cli_$cfg.log"; return $rc ;;
+    *) echo "unknown step $s"; return 2 ;;
+  esac
+}
+
+for s in "$@"; do
+  echo "== $s ($(date +%T))"
+  step "$s" || { echo "step $s failed"; exit 1; }
+done
+echo "session $TAG done"
