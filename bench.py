@@ -94,9 +94,10 @@ def cpu_baseline(threads: int | None = None, sample_j1: int = 60):
     scalar POA, with ccsx's chunked pipeline and -j threads (kt_for dynamic
     sharing).  It stands in for `ccsx -A -j N`, unbuildable here (bsalign is
     not vendored): a scalar C restatement, not bsalign's SIMD code.
-    -j N uses the process's CPU share (min(affinity, 16): the GPU box gives
-    16 host CPUs per GPU, while nproc reports the whole machine); -j 1 runs on
-    a `sample_j1`-ZMW prefix for the per-core rate."""
+    -j N = every CPU of the process's affinity mask (the reference's -j goes
+    straight to kt_for, main.c:794-795, kthread.c:48-65), uncapped; the line
+    records the affinity count beside nproc.  -j 1 runs on a `sample_j1`-ZMW
+    prefix for the per-core rate."""
     import subprocess
     import tempfile
     from tools.gen_synth import write
@@ -104,8 +105,9 @@ def cpu_baseline(threads: int | None = None, sample_j1: int = 60):
     if not os.path.exists(exe):
         from ccsx_amd.build import build_oracle
         build_oracle()
+    affinity = len(os.sched_getaffinity(0))
     if threads is None:
-        threads = max(1, min(len(os.sched_getaffinity(0)), 16))
+        threads = max(1, affinity)
     d = tempfile.mkdtemp(prefix="ccsx_cpu_")
     fa, fa1 = os.path.join(d, "a.fa"), os.path.join(d, "a1.fa")
     write(fa, 1000, 10000, 8, seed=SEED)
@@ -124,11 +126,12 @@ def cpu_baseline(threads: int | None = None, sample_j1: int = 60):
     for f in os.listdir(d):
         os.remove(os.path.join(d, f))
     os.rmdir(d)
-    return {"value": round(n / dt, 3), "unit": "ZMWs/s", "cores": threads, "kind": "port",
+    return {"value": round(n / dt, 3), "unit": "ZMWs/s", "cores": threads, "affinity": affinity,
+            "nproc": os.cpu_count(), "kind": "port",
             "per_core_zmws_per_s": round(n1 / dt1, 3), "wall_s": round(dt, 3),
             "sample": f"config A end to end: {n} CCS from 1,000 ZMWs (10 kb x 8 passes, 10% error) read from FASTA, "
-                      f"ccs_prepare, POA and ordered output by oracle/ccsx_cpu -A -j {threads} (the box's CPU share; "
-                      f"nproc={os.cpu_count()}) in {dt:.2f} s; -j 1 on the first {sample_j1} ZMWs: {n1 / dt1:.2f} ZMWs/s. "
+                      f"ccs_prepare, POA and ordered output by oracle/ccsx_cpu -A -j {threads} (every CPU of the "
+                      f"process's affinity mask: {affinity}; nproc={os.cpu_count()}) in {dt:.2f} s; -j 1 on the first {sample_j1} ZMWs: {n1 / dt1:.2f} ZMWs/s. "
                       "A scalar C restatement of SPEC.md + main.c, not bsalign's SIMD code (ccsx itself is "
                       "unbuildable here)"}
 

@@ -31,16 +31,6 @@
 
 namespace ccsx_ingest {
 
-namespace {
-
-// decompressed bytes per block (CCSX_INGEST_BLOCK overrides it: the tests
-// use a few bytes so every record crosses blocks) and the headroom in front
-// of each block for the carried tail of the previous one
-size_t g_block = 32u << 20;
-size_t head_bytes() { return std::min<size_t>(2u << 20, 4 * g_block); }
-
-}  // namespace
-
 struct Block {
     std::unique_ptr<char[]> mem;
     size_t cap = 0;
@@ -53,10 +43,11 @@ struct Block {
     {
         if (map) munmap(map, map_len);
     }
-    static std::shared_ptr<Block> make(size_t payload)
+    // `head` bytes of headroom in front of the payload for the carried tail
+    // of the previous block
+    static std::shared_ptr<Block> make(size_t payload, size_t head)
     {
         auto b = std::make_shared<Block>();
-        const size_t head = head_bytes();
         b->cap = head + payload;
         b->mem.reset(new char[b->cap]);
         b->data = b->mem.get() + head;
@@ -68,6 +59,10 @@ namespace {
 
 // ---------------------------------------------------------------- byte sources
 struct ByteSource {
+    // decompressed bytes per block (CCSX_INGEST_BLOCK overrides it per
+    // source: the tests use a few bytes so every record crosses blocks)
+    size_t block = 32u << 20;
+    size_t head() const { return std::min<size_t>(2u << 20, 4 * block); }
     virtual ~ByteSource() = default;
     // next block of decompressed bytes (len may be 0 only with eof)
     virtual std::shared_ptr<Block> next() = 0;
@@ -84,9 +79,9 @@ struct FdSource : ByteSource {
     }
     std::shared_ptr<Block> next() override
     {
-        auto b = Block::make(g_block);
-        while (!done && b->len < g_block) {
-            const ssize_t r = read(fd, b->data + b->len, g_block - b->len);
+        auto b = Block::make(block, head());
+        while (!done && b->len < block) {
+            const ssize_t r = read(fd, b->data + b->len, block - b->len);
             if (r <= 0) done = true;
             else b->len += (size_t)r;
         }
@@ -136,9 +131,9 @@ struct GzSource : ByteSource {
     ~GzSource() override { gzclose(fp); }
     std::shared_ptr<Block> next() override
     {
-        auto b = Block::make(g_block);
-        while (!done && b->len < g_block) {
-            const int r = gzread(fp, b->data + b->len, (unsigned)std::min<size_t>(g_block - b->len, 1u << 30));
+        auto b = Block::make(block, head());
+        while (!done && b->len < block) {
+            const int r = gzread(fp, b->data + b->len, (unsigned)std::min<size_t>(block - b->len, 1u << 30));
             if (r <= 0) done = true;
             else b->len += (size_t)r;
         }
@@ -176,7 +171,9 @@ struct BgzfSource : ByteSource {
         }
         return in.size() >= need;
     }
-    // size of the member at ipos (0 = end or not BGZF)
+    // size of the member at ipos (0 = end, not BGZF, or a header that does
+    // not describe a whole member: every subfield inside XLEN, BSIZE + 1 at
+    // least the header and the 8-byte trailer)
     size_t member_size()
     {
         if (!fill(18)) return 0;
@@ -187,7 +184,11 @@ struct BgzfSource : ByteSource {
         h = in.data() + ipos;
         for (size_t x = 12; x + 4 <= 12 + xlen;) {
             const size_t sl = h[x + 2] | (size_t)h[x + 3] << 8;
-            if (h[x] == 66 && h[x + 1] == 67 && sl == 2) return (h[x + 4] | (size_t)h[x + 5] << 8) + 1;
+            if (x + 4 + sl > 12 + xlen) return 0;
+            if (h[x] == 66 && h[x + 1] == 67 && sl == 2) {
+                const size_t sz = (h[x + 4] | (size_t)h[x + 5] << 8) + 1;
+                return sz >= 12 + xlen + 8 ? sz : 0;
+            }
             x += 4 + sl;
         }
         return 0;
@@ -203,7 +204,7 @@ struct BgzfSource : ByteSource {
             in.erase(in.begin(), in.begin() + (ptrdiff_t)ipos);
             ipos = 0;
         }
-        while (!done && total < g_block) {
+        while (!done && total < block) {
             const size_t sz = member_size();
             if (!sz || !fill(sz)) {
                 // end of input (a partial or foreign member ends it, as a
@@ -214,12 +215,16 @@ struct BgzfSource : ByteSource {
             }
             const unsigned char *t = in.data() + ipos + sz - 4;
             const size_t isize = t[0] | (size_t)t[1] << 8 | (size_t)t[2] << 16 | (size_t)t[3] << 24;
+            if (isize > 65536) {  // a BGZF member inflates to at most 64 KiB
+                bad = done = true;
+                break;
+            }
             ms.push_back({ipos, sz, total, isize});
             total += isize;
             ipos += sz;
             if (ipos > (64u << 20)) break;  // keep the compressed window bounded
         }
-        auto b = Block::make(std::max<size_t>(total, 1));
+        auto b = Block::make(std::max<size_t>(total, 1), head());
         b->len = total;
         std::atomic<size_t> nx(0);
         std::atomic<bool> err(false);
@@ -340,7 +345,7 @@ public:
             memcpy(nb->data, cur_->data + keep_from, tail);
             nb->len += tail;
         } else {
-            auto big = Block::make(tail + nb->len);
+            auto big = Block::make(tail + nb->len, nb->mem ? (size_t)(nb->data - nb->mem.get()) : 0);
             memcpy(big->data, cur_->data + keep_from, tail);
             memcpy(big->data + tail, nb->data, nb->len);
             big->len = tail + nb->len;
@@ -380,7 +385,9 @@ uint32_t seq_lines(const char *b, size_t n, std::string *out)
         if (STORE) out->append(b + q - 1, L);
         len += L;
         last = b[le - 1];
-        if (len > 1 && last == '\r') {
+        // (kseq strips a line's '\r' in ks_getuntil2, which returns before
+        // the strip when the line's first char was the input's last byte)
+        if (len > 1 && last == '\r' && (L > 1 || nl)) {
             --len;
             last = L >= 2 ? b[le - 2] : prev;
             if (STORE) out->pop_back();
@@ -528,7 +535,7 @@ private:
             const char prev = last;
             len += L;
             last = b[le - 1];
-            if (len > 1 && last == '\r') --len, last = L >= 2 ? b[le - 2] : prev;
+            if (len > 1 && last == '\r' && (L > 1 || nl)) --len, last = L >= 2 ? b[le - 2] : prev;
             if (++nlines == 1) ls = q - 1, ll = L;
             q = nl ? le + 1 : n;
         }
@@ -732,7 +739,7 @@ private:
 std::unique_ptr<ZmwSource> ZmwSource::open(const char *path, bool is_bam, int nthreads)
 {
     const char *e = getenv("CCSX_INGEST_BLOCK");
-    g_block = e ? (size_t)std::max<long>(1, atol(e)) : (32u << 20);
+    const size_t block = e ? (size_t)std::max<long>(1, atol(e)) : (32u << 20);
     std::unique_ptr<ByteSource> src;
     if (strcmp(path, "-") == 0) {
         gzFile g = gzdopen(dup(0), "rb");
@@ -766,6 +773,7 @@ std::unique_ptr<ZmwSource> ZmwSource::open(const char *path, bool is_bam, int nt
                 src.reset(new FdSource(fd));
         }
     }
+    src->block = block;
     std::unique_ptr<RecordReader> rr;
     if (is_bam) rr.reset(new BamReader(std::move(src)));
     else rr.reset(new FxReader(std::move(src)));

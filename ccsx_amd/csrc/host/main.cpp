@@ -245,6 +245,38 @@ private:
     bool eof_ = false, stop_ = false;
 };
 
+// -X (main.c:772-782): each option kputs-appends its argument to one buffer,
+// then ksplit(',') splits the buffer *as a C string* in place (kstring.c:
+// 65-107: a field's end delimiter becomes NUL, empty fields are skipped) and
+// a fresh hole set holds the fields.  So only the last -X's set counts, and
+// after a first split the buffer's C string ends at the first field: `-X 3,5
+// -X 7` excludes hole 3, `-X 3 -X 7` excludes hole 37.
+std::unordered_set<std::string> exclude_holes(std::string &buf, const char *arg)
+{
+    buf.append(arg);
+    const size_t l = strnlen(buf.data(), buf.size());
+    std::unordered_set<std::string> set;
+    std::vector<size_t> starts;
+    char last = 0;
+    size_t start = 0;
+    for (size_t i = 0; i <= l; ++i) {
+        const char ch = i < l ? buf[i] : '\0';
+        if (ch == ',' || ch == '\0') {
+            if (last != 0 && last != ',') {
+                if (i < l) buf[i] = '\0';
+                starts.push_back(start);
+                last = '\0';
+                continue;
+            }
+        } else if (last == ',' || last == 0) {
+            start = i;
+        }
+        last = ch;
+    }
+    for (size_t st : starts) set.insert(std::string(buf.c_str() + st));
+    return set;
+}
+
 }  // namespace
 
 int main(int argc, char **argv)
@@ -252,6 +284,7 @@ int main(int argc, char **argv)
     int c, verbose = 0, min_subread_len = 5000, max_subread_len = 500000, min_fulllen_count = 3, nthreads = 1;
     int isbam = 1, split_subread = 1;
     std::unordered_set<std::string> hole_set;
+    std::string xbuf;  // -X: kputs-appended, ksplit in place (exclude_holes)
     bool have_holes = false;
     while ((c = getopt(argc, argv, "hm:M:c:j:X:PAv")) != -1) {
         switch (c) {
@@ -259,19 +292,10 @@ int main(int argc, char **argv)
         case 'M': max_subread_len = atoi(optarg); break;
         case 'P': split_subread = 0; break;
         case 'A': isbam = 0; break;
-        case 'X': {  // main.c:772-782 (ksplit on ',': empty fields skipped)
+        case 'X':  // main.c:772-782
             have_holes = true;
-            std::string s(optarg), f;
-            for (size_t i = 0; i <= s.size(); ++i) {
-                if (i == s.size() || s[i] == ',') {
-                    if (!f.empty()) hole_set.insert(f);
-                    f.clear();
-                } else {
-                    f.push_back(s[i]);
-                }
-            }
+            hole_set = exclude_holes(xbuf, optarg);
             break;
-        }
         case 'c':
             min_fulllen_count = atoi(optarg);
             if (min_fulllen_count < 3) {

@@ -117,3 +117,19 @@ def test_cli_verbose_segments(tmp_path):
     err = r.stderr.decode()
     assert err.count(" strand=") == 12
     assert ">0_0/6 strand=0 len=" in err
+
+
+@pytest.mark.parametrize("xargs,excluded", [(["-X", "3,5", "-X", "7"], {"3"}), (["-X", "3", "-X", "7"], {"37"}),
+                                            (["-X", "1,,2,"], {"1", "2"})])
+def test_cli_repeated_exclude(tmp_path, xargs, excluded):
+    """-X as main.c:772-782 builds it: each option kputs-appends to one buffer
+    that ksplit then splits as a C string in place, and a fresh hole set takes
+    the fields, so only the last -X counts and it sees the first field of the
+    earlier ones joined with its own text."""
+    fa = str(tmp_path / "in.fa")
+    write(fa, 40, 1000, 6)
+    out = str(tmp_path / "out.fa")
+    _run(["-A", "-j", "4"] + xargs + [fa, out])
+    got = open(out, "rb").read()
+    assert got == _expected(fa, 0, exclude=excluded)
+    assert got.count(b">") == 40 - len(excluded)

@@ -3,7 +3,8 @@
 # timing (tools/gpu_ab.sh).  The flags go to every kernel configuration
 # (after its own defines, so they override them) and to the host launcher;
 # the configurations' defines come from ccsx_amd/build.py (KCFGS).
-#   tools/build_variant.sh TAG -DFOO=1 ...
+#   [CFGS="tput occ"] tools/build_variant.sh TAG -DFOO=1 ...
+# CFGS limits the extra flags to the named configurations (default: all).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TAG=$1; shift
@@ -13,12 +14,16 @@ INC="-I$ROOT/include -I$C -I$C/host"
 K="/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC -mllvm -amdgpu-sched-strategy=max-ilp -Wno-macro-redefined"
 KOBJS=""
 while read -r NAME DEFS; do
-  $K $DEFS "$@" -c $C/ccsx_kernel.hip -o $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o &
+  X=("$@")
+  [ -n "$CFGS" ] && [[ " $CFGS " != *" $NAME "* ]] && X=()
+  rm -f $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o
+  $K $DEFS "${X[@]}" -c $C/ccsx_kernel.hip -o $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o &
   KOBJS="$KOBJS $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o"
 done < <(cd "$ROOT" && python3 -c "from ccsx_amd.build import KCFGS; [print(n, ' '.join(d)) for n, d in KCFGS]")
 /opt/rocm/bin/hipcc -x c++ -O3 -std=c++17 -fPIC $INC -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include "$@" \
   -c $C/ccsx_gpu.cpp -o $OBJ/ccsx_gpu_$TAG.cpp.o
 wait
+for o in $KOBJS; do [ -f $o ] || { echo "kernel object $o failed"; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/ccsx_amd/libccsx_amd_$TAG.so $KOBJS \
   $OBJ/ccsx_gpu_$TAG.cpp.o $OBJ/bspoa_gpu.cpp.o $OBJ/prepare.cpp.o $OBJ/pairwise.cpp.o \
   $OBJ/seqio.cpp.o $OBJ/dispatch.cpp.o $OBJ/ingest.cpp.o -lz -lpthread

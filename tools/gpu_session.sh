@@ -12,7 +12,9 @@
 #   ab:CFG:KCFG,...    interleaved rounds of bench --config CFG over several kernel cfgs
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
+#   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
 #   cli:N              CLI end to end on N config-E ZMWs streamed on stdin (tools/cli_e2e.py)
+#   lib:NAME           the following steps load ccsx_amd/NAME (CCSX_LIB); lib: resets
 # Environment: CCSX_LIB selects a library variant for the bench steps.
 set -o pipefail
 TAG=$1; shift
@@ -43,7 +45,7 @@ step() {
         timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" && cat "$OUT/bench.json"
         return $?
       fi
-      local f="$OUT/bench_${cfg}${k:+_k$k}.json"
+      local f="$OUT/bench_${cfg}${k:+_k$k}${CCSX_LIB:+_${CCSX_LIB%.so}}.json"
       timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$k") > "$f" 2> "${f%.json}.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['value'], 'ZMWs/s', d['gcups'], 'GCUPS', 'cfg', d['roofline'].get('kernel_cfg'))" "$f" ;;
     ab)
@@ -61,9 +63,16 @@ step() {
         echo "kt $cfg done" ;;
     pmc)
       timeout -k 10 900 bash "$R/tools/pmc_pass.sh" "$TAG/pmc_$cfg" --config "$cfg" > "$OUT/pmc_$cfg.log" 2>&1 && echo "pmc $cfg done" ;;
+    phase)  # phase:L,PASSES,N:KCFG  (per-ZMW cycle split; CCSX_LIB=libccsx_amd_diag.so for the DP detail)
+      local L P N; IFS=, read -r L P N <<< "$cfg"
+      timeout -k 10 600 python -u tools/phase_prof.py --L "$L" --passes "$P" --n "$N" --kcfg "${k:--1}" \
+        > "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" 2> "$OUT/phase.err" &&
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['kernel_ms'],2), 'ms', d['share'], d.get('two_wave'))" "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" ;;
     cli)
       timeout -k 10 900 python -u tools/cli_e2e.py --n "$cfg" --out "$OUT" > "$OUT/cli_$cfg.log" 2>&1; local rc=$?
       tail -5 "$OUT/cli_$cfg.log"; return $rc ;;
+    lib)  # lib:NAME -- later steps load ccsx_amd/NAME (lib: = the product library)
+      if [ -n "$cfg" ]; then export CCSX_LIB=$cfg; else unset CCSX_LIB; fi ;;
     *) echo "unknown step $s"; return 2 ;;
   esac
 }

@@ -135,6 +135,11 @@ def cases():
     body = b"".join(b"@%s\n%s\n+\n%s\n%s\n" % (n.encode(), s.encode(), (b"@" + b">" * (len(s) // 2 - 1)),
                                                   b"I" * (len(s) - len(s) // 2)) for n, s in fq)
     c["fq_quirks.fq"] = (0, body + b"@mvq/16/0_0\n+\nIII\n" + fastq(zmw("mvq", 17, 3, 25)))
+    # the input's last byte is a '\r' that starts a line: kseq's ks_getuntil2
+    # returns before its '\r' strip, so the '\r' stays a base; a last line of
+    # two or more chars without a newline is stripped as usual
+    c["cr_last_line.fa"] = (0, fasta(zmw("mv", 18, 3, 20)) + b"\r")
+    c["cr_last_line2.fa"] = (0, fasta(zmw("mv", 19, 3, 20))[:-1] + b"\r")
     c["basic.bam"] = (1, bam(base))
     c["bgzf.bam"] = (1, bgzf(bam_raw(base + zmw("mvb", 21, 6, 3000))))
     c["bgzf.fa.gz"] = (0, bgzf(fasta(base + zmw("mvb", 22, 5, 4000), width=61)))
@@ -150,7 +155,9 @@ def run_ref(exe, isbam, path):
 
 def parse(out):
     res = []
-    for line in out.splitlines():
+    for line in out.split("\n"):  # (not splitlines: a base may be '\r')
+        if not line:
+            continue
         f = line.split("\t")
         if len(f) == 1:
             res.append({"ret": int(f[0])})

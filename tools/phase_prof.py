@@ -7,9 +7,12 @@ ap.add_argument("--L", type=int, default=10000)
 ap.add_argument("--passes", type=int, default=8)
 ap.add_argument("--n", type=int, default=1000)
 ap.add_argument("--mode", type=int, default=0)
+ap.add_argument("--kcfg", type=int, default=-1, help="force a kernel configuration (ccsx_layout.h KernelCfg)")
 a = ap.parse_args()
 zs = [cx.prepare(cx.synth_zmw(20201104, h, a.L, a.passes)[0]) for h in range(a.n)]
 e = cx.Engine(0)
+if a.kcfg >= 0:
+    e.set_kernel_cfg(a.kcfg)
 e.stage(zs)
 e.launch(a.mode)
 e.set_profiling(True)
