@@ -48,8 +48,19 @@ def lib() -> C.CDLL:
                                      C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.POINTER(C.c_uint32)),
                                      C.POINTER(C.c_uint32), C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
                                      C.POINTER(C.c_uint64)]
+        L.ocsx_edit_distance.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32]
+        L.ocsx_edit_distance.restype = C.c_int64
         _lib = L
     return _lib
+
+
+def edit_identity(a: bytes, b: bytes, band: int = 1024) -> float:
+    """1 - (banded) edit distance / max length: a lower bound of the identity
+    (accuracy sanity check vs synthetic truth; not parity)."""
+    if not a or not b:
+        return 0.0
+    d = lib().ocsx_edit_distance(a, len(a), b, len(b), band)
+    return 0.0 if d < 0 else 1.0 - d / max(len(a), len(b))
 
 
 class Poa:

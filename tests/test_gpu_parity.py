@@ -7,7 +7,7 @@ BASELINE sizes are covered by test_gpu_full_size_properties.
 import pytest
 
 import ccsx_amd as cx
-from oracle.oracle import Poa, batch
+from oracle.oracle import Poa, batch, edit_identity
 from tests.zmw_cases import edge_cases, high_indegree, raw, synth
 
 pytestmark = pytest.mark.gpu
@@ -69,10 +69,16 @@ def test_repeat_launch_deterministic(engine):
     assert a == b
 
 
+def _identity(ccs, ins):
+    """CCS vs the generator's true insert, either strand (the template may be
+    a reverse pass): a banded edit identity (not parity)."""
+    return max(edit_identity(ccs, ins), edit_identity(ccs, cx.revcomp(ins)))
+
+
 def test_gpu_full_size_properties(engine):
     """BASELINE config B shape (10 kb x 8) at a 64-ZMW sample: parity on a
-    subset plus size-independent properties on all (status, length, identity
-    to the synthetic truth)."""
+    subset plus size-independent properties on all: status, length, cells and
+    identity to the synthetic truth (mean >= 0.99, min >= 0.985)."""
     import random
     zs, truth = [], []
     for h in range(64):
@@ -80,14 +86,52 @@ def test_gpu_full_size_properties(engine):
         zs.append(cx.prepare(subs))
         truth.append(ins)
     got = engine.run(zs, cx.MODE_SHRED)
+    ids = []
     for (g, status, cells), ins in zip(got, truth):
         assert status == 0
         assert 9700 <= len(g) <= 10300
         assert cells > 8_000_000
+        ids.append(_identity(g, ins))
+    assert sum(ids) / len(ids) >= 0.99 and min(ids) >= 0.985, (sum(ids) / len(ids), min(ids))
     sample = random.Random(3).sample(range(64), 6)
     want, _, _ = batch([zs[i] for i in sample], cx.MODE_SHRED, 6)
     for i, w in zip(sample, want):
         assert got[i][0] == w
+
+
+def _config_shapes(name, n):
+    import bench
+    if name == "E":
+        cfg = bench.CONFIGS["E"]
+        holes = range(10_000_000, 10_000_000 + 4000)
+        shapes = sorted(((h, *bench.zmw_shape(cfg, h)) for h in holes), key=lambda s: s[1] * s[2])
+        # the smallest, the median and the largest drawn shapes
+        return [shapes[0], shapes[len(shapes) // 2], shapes[-1]] + [shapes[i * 37 % len(shapes)] for i in range(n - 3)]
+    L, p = {"C": (20000, 5), "D": (2000, 30)}[name]
+    return [(20_000 + h, L, p) for h in range(n)]
+
+
+@pytest.mark.parametrize("name,mode,n", [("C", cx.MODE_PRIMITIVE, 24), ("D", cx.MODE_SHRED, 48), ("E", cx.MODE_SHRED, 24)])
+def test_gpu_accuracy_vs_truth(engine, name, mode, n):
+    """Configs C (20 kb x 5, -P, main.c:486-502), D (2 kb x 30) and E (mixed
+    5-25 kb inserts x 5-12 passes, shredded, main.c:622-638): the device's
+    CCS against the synthetic truth (mean >= 0.99, min >= 0.985), plus oracle
+    parity on a 3-ZMW sample.  A restatement that is deterministic but
+    degrades at these lengths or pass counts fails here."""
+    import bench
+    zs, truth = [], []
+    for h, L, p in _config_shapes(name, n):
+        subs, ins = cx.synth_zmw(bench.SEED, h, L, p)
+        zs.append(cx.prepare(subs))
+        truth.append(ins)
+    got = engine.run(zs, mode)
+    ids = []
+    for (g, status, _), ins in zip(got, truth):
+        assert status == 0
+        ids.append(_identity(g, ins))
+    assert sum(ids) / len(ids) >= 0.99 and min(ids) >= 0.985, (sum(ids) / len(ids), min(ids))
+    want, _, _ = batch(zs[:3], mode, 3)
+    assert [g for g, _, _ in got[:3]] == want
 
 
 @pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])

@@ -101,3 +101,25 @@ def test_golden_vectors():
         out = Poa().zmw(p.seqs, p.offs, p.lens, case["mode"])
         assert len(out) == case["len"]
         assert hashlib.sha256(out).hexdigest() == case["sha256"]
+
+
+def test_edit_identity_known_answers():
+    """The accuracy checks' banded edit identity (oracle/poa_identity.c)
+    against the exact numpy distance above."""
+    import random
+    from oracle.oracle import edit_identity
+    rnd = random.Random(5)
+    for _ in range(20):
+        a = bytes(rnd.choice(b"ACGT") for _ in range(rnd.randint(50, 400)))
+        b = bytearray(a)
+        for _ in range(rnd.randint(0, 30)):
+            k = rnd.randrange(len(b))
+            op = rnd.randrange(3)
+            if op == 0:
+                b[k] = rnd.choice(b"ACGT")
+            elif op == 1:
+                del b[k]
+            else:
+                b.insert(k, rnd.choice(b"ACGT"))
+        assert abs(edit_identity(a, bytes(b)) - _edit_identity(a, bytes(b))) < 1e-12
+    assert edit_identity(b"", b"ACGT") == 0.0
