@@ -158,6 +158,13 @@ struct ccsx_ctx {
     bool shred_caps = false;           // tight caps sized for shredding windows (ccsx_gpu_run, shredded mode)
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
     bool prealloc = false;             // reserve the slice budget up front
+    bool bp_log = false;               // record the -v >= 3 breakpoint log (main.c:619-620)
+    uint64_t bp_words = 0;             // words of the staged slice's breakpoint log
+    DevBuf d_bp;
+    std::vector<uint32_t> h_bp;
+    std::vector<uint32_t> run_bp;      // ccsx_gpu_run: the gathered logs, (i, ncols) pairs
+    std::vector<uint64_t> run_bp_off;  // per ZMW of the call: offset into run_bp (pairs)
+    std::vector<uint32_t> run_bp_n;    // per ZMW of the call: rounds
     std::vector<uint8_t> run_arena;    // ccsx_gpu_run's gathered CCS strings
     DevBuf d_prof;
     std::vector<unsigned long long> h_prof;
@@ -220,7 +227,7 @@ void ccsx_gpu_close(ccsx_ctx *c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    DevBuf *bufs[] = {&c->d_prof, &c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_order, &c->d_ws, &c->d_out,
+    DevBuf *bufs[] = {&c->d_bp, &c->d_prof, &c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_order, &c->d_ws, &c->d_out,
                       &c->d_msa, &c->d_olen, &c->d_ncols, &c->d_status, &c->d_cells};
     for (DevBuf *b : bufs) b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -243,6 +250,7 @@ const char *ccsx_gpu_status_str(int32_t s)
     case ccsx::kErrReadLen: return "read longer than the LDS read buffer";
     case ccsx::kErrOut: return "consensus longer than the output slab";
     case ccsx::kErrTrace: return "traceback did not terminate";
+    case ccsx::kErrBpLog: return "more shredding rounds than the breakpoint log holds";
     default: return "unknown status";
     }
 }
@@ -300,7 +308,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, hipSetDevice(c->device));
     c->nz = nz;
     c->desc.assign(nz, ccsx::ZmwDesc{});
-    uint64_t seq_b = 0, ws_b = 0, out_b = 0, msa_b = 0;
+    uint64_t seq_b = 0, ws_b = 0, out_b = 0, msa_b = 0, bp_w = 0;
     uint32_t nseg = 0, lmax_all = 0, nmax = 0;
     for (size_t i = 0; i < nz; ++i) {
         const ccsx_zmw_in &zi = z[i];
@@ -325,11 +333,18 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
         d.msa_off = msa_b;
         d.msacap = with_msa ? uint32_t((S + 16) * (zi.nseg + 4)) : 0u;
         msa_b += d.msacap;
+        // breakpoint log: a round emits >= 1 column and advances >= 1 read
+        // cursor, so S + 2 rounds bound any ZMW (full caps); tight caps hold
+        // far more than the ~L / 1,900 rounds of a real one
+        d.bpcap = c->bp_log ? (full_caps ? uint32_t(S + 2) : uint32_t(S / 512 + 64)) : 0u;
+        d.bp_off = bp_w;
+        bp_w += c->bp_log ? 1 + 2 * uint64_t(d.bpcap) : 0;
         nseg += zi.nseg;
         lmax_all = std::max(lmax_all, lmax);
         nmax = std::max(nmax, zi.nseg);
     }
     c->seq_bytes = seq_b, c->ws_bytes = ws_b, c->out_bytes = out_b, c->msa_bytes = msa_b;
+    c->bp_words = bp_w;
     c->nseg_total = nseg;
     // nibble-pair read buffer (ccsx_kernel.hip load_read); at least one band:
     // every lane reads its window bytes even when the read is shorter.  A
@@ -382,6 +397,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     HIPCHK(c, c->d_ncols.reserve(nz * 4));
     HIPCHK(c, c->d_status.reserve(nz * 4));
     HIPCHK(c, c->d_cells.reserve(nz * 8));
+    if (bp_w) HIPCHK(c, c->d_bp.reserve(bp_w * 4));
     const auto tb = std::chrono::steady_clock::now();
     // host staging of the sequence arena and segment tables
     HIPCHK(c, c->h_seq.reserve(seq_b, c->prealloc ? kPinnedFloor : 0));
@@ -449,6 +465,7 @@ int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
     a.lds_read_words = c->lds_read_words;
     a.lds_nmax = c->lds_nmax;
     a.prof = nullptr;
+    a.bplog = c->bp_words ? c->d_bp.as<uint32_t>() : nullptr;
     if (c->profiling) {
         HIPCHK(c, c->d_prof.reserve(c->nz * ccsx::kProfSlots * 8));
         a.prof = c->d_prof.as<unsigned long long>();
@@ -491,6 +508,9 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
         HIPCHK(c, hipMemcpyAsync(c->h_status.data(), c->d_status.p, nz * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_cells.data(), c->d_cells.p, nz * 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_out.p, c->d_out.p, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+        c->h_bp.resize(c->bp_words);
+        if (c->bp_words)
+            HIPCHK(c, hipMemcpyAsync(c->h_bp.data(), c->d_bp.p, c->bp_words * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     int bad = 0;
@@ -514,7 +534,7 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
 static bool is_cap_error(int32_t s)
 {
     return s == ccsx::kErrRows || s == ccsx::kErrEdges || s == ccsx::kErrMulti || s == ccsx::kErrSpill ||
-           s == ccsx::kErrReadLen;
+           s == ccsx::kErrReadLen || s == ccsx::kErrBpLog;
 }
 
 // One chunk.  The chunk is cut into slices that fit the device's free memory
@@ -558,6 +578,9 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     }
     c->run_arena.clear();
+    c->run_bp.clear();
+    c->run_bp_off.assign(nz, 0);
+    c->run_bp_n.assign(nz, 0);
     std::vector<uint64_t> aoff(nz, 0);
     std::vector<int> cls(nz, 0);
     std::string first_err;
@@ -609,6 +632,12 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
                 aoff[g] = c->run_arena.size();
                 out[g].len = o[i].len;
                 c->run_arena.insert(c->run_arena.end(), o[i].ccs, o[i].ccs + o[i].len);
+                if (c->bp_words && mode == CCSX_MODE_SHRED) {
+                    const uint32_t *lg = c->h_bp.data() + c->desc[i].bp_off;
+                    c->run_bp_off[g] = c->run_bp.size() / 2;
+                    c->run_bp_n[g] = lg[0];
+                    c->run_bp.insert(c->run_bp.end(), lg + 1, lg + 1 + 2 * uint64_t(lg[0]));
+                }
             }
             b = e;
         }
@@ -673,6 +702,21 @@ int ccsx_gpu_set_mem_share(ccsx_ctx *c, uint32_t share)
 {
     if (!c || share == 0) return -1;
     c->mem_share = share;
+    return 0;
+}
+
+int ccsx_gpu_set_bp_log(ccsx_ctx *c, int on)
+{
+    if (!c) return -1;
+    c->bp_log = on != 0;
+    return 0;
+}
+
+int ccsx_gpu_bp_log(const ccsx_ctx *c, size_t zmw, const uint32_t **pairs, uint32_t *nrounds)
+{
+    if (!c || zmw >= c->run_bp_n.size()) return -1;
+    *nrounds = c->run_bp_n[zmw];
+    *pairs = c->run_bp.data() + 2 * c->run_bp_off[zmw];
     return 0;
 }
 

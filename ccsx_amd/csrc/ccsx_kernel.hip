@@ -918,6 +918,12 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
     }
 }
 
+// helper rows per straight-line group (dpB_group); 0: one row at a time
+#ifndef CCSX_HGROUP
+#define CCSX_HGROUP 2
+#endif
+constexpr int kHGroup = CCSX_HGROUP;
+
 // helper wave: everything after the predecessor terms of row r (SPEC.md
 // §3.2-§3.5): M, H', the insertion scan, the cell codes and tags, the
 // free-end candidates, the record store
@@ -966,8 +972,13 @@ __device__ __forceinline__ void dpB_tail(Z &z, BState &S, uint32_t r, uint32_t m
     // lexicographic (max e, min row, min cell): rows may come out of order
     // (dpB_group: the other rows after the group's simple ones)
     const uint32_t k0 = r * 2u, k1 = k0 + 1u;
-    if (e0 > S.bE || (e0 == S.bE && k0 < S.bKey)) S.bE = e0, S.bKey = k0, S.bOff = off;
-    if (e1 > S.bE || (e1 == S.bE && k1 < S.bKey)) S.bE = e1, S.bKey = k1, S.bOff = off;
+    if (kHGroup == 0) {  // rows in order: the first maximum is the earliest
+        if (e0 > S.bE) S.bE = e0, S.bKey = k0, S.bOff = off;
+        if (e1 > S.bE) S.bE = e1, S.bKey = k1, S.bOff = off;
+    } else {
+        if (e0 > S.bE || (e0 == S.bE && k0 < S.bKey)) S.bE = e0, S.bKey = k0, S.bOff = off;
+        if (e1 > S.bE || (e1 == S.bE && k1 < S.bKey)) S.bE = e1, S.bKey = k1, S.bOff = off;
+    }
     // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
     __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), S.rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
                                           0);
@@ -1031,11 +1042,6 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
 // ext iff D > a of the chosen slot).  Any other row of the group is left to
 // dpB_row afterwards (the free-end candidates compare lexicographically, so
 // the order does not matter).
-#ifndef CCSX_HGROUP
-#define CCSX_HGROUP 2
-#endif
-constexpr int kHGroup = CCSX_HGROUP;
-
 template <bool FULL, int G>
 __device__ __forceinline__ void dpB_group(Z &z, BState &S, uint32_t r0, uint32_t st, uint32_t m, int32_t lim,
                                           int32_t vOff, const LaneK &c)
@@ -1148,12 +1154,20 @@ __device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t
     const int32_t lim = FULL ? (int32_t)m - kW : 0;
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
-    // this helper's rows r0 + h + kHelpers i, in groups of kHGroup
+    // this helper's rows r0 + h + kHelpers i, in groups of kHGroup (0: one
+    // row at a time)
     constexpr int kRowsPerHelper = kBlkAB / kHelpers;
-    static_assert(kRowsPerHelper % kHGroup == 0, "a helper's rows of a block form whole groups");
+    if (kHGroup == 0) {
 #pragma unroll
-    for (int g = 0; g < kRowsPerHelper; g += kHGroup)
-        dpB_group<FULL, kHGroup>(z, S, r0 + h + (uint32_t)(g * kHelpers), kHelpers, m, lim, vOff, c);
+        for (uint32_t i = h; i < (uint32_t)kBlkAB; i += kHelpers)
+            if (r0 + i < R) dpB_row<FULL>(z, S, r0 + i, m, lim, vOff, c);
+    } else {
+        constexpr int G = kHGroup ? kHGroup : 1;
+        static_assert(kRowsPerHelper % G == 0, "a helper's rows of a block form whole groups");
+#pragma unroll
+        for (int g = 0; g < kRowsPerHelper; g += G)
+            dpB_group<FULL, G>(z, S, r0 + h + (uint32_t)(g * kHelpers), kHelpers, m, lim, vOff, c);
+    }
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
     if (h == 0 && ((r0 & 15u) == 16u - kBlkAB || rend == R)) {
         const uint32_t g0 = r0 & ~15u;
@@ -2471,6 +2485,7 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
         for (uint32_t k = lane; k < n; k += 64) z.pos[k] = 0;
         wsync();
         bool flag = true;
+        uint32_t nround = 0;  // shredding rounds (the -v >= 3 breakpoint log)
         while (flag && !z.status) {
             uint32_t i = 0, ncols = 0;
             for (uint32_t ws = initlen;; ws += addlen) {
@@ -2495,9 +2510,21 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
                 if (i >= 1) break;
             }
             if (z.status) break;
+            if (a.bplog) {
+                // main.c:619-620: "breakpoint=i maplen=ncols" (the host prints it)
+                if (lane == 0 && nround < z.d.bpcap) {
+                    a.bplog[z.d.bp_off + 1 + 2 * nround] = i;
+                    a.bplog[z.d.bp_off + 2 + 2 * nround] = ncols;
+                }
+                ++nround;
+            }
             const unsigned long long te0 = stamp();
             emit(z, i, ncols, n, flag, out, ol);
             z.pf[kPfShred] += stamp() - te0;
+        }
+        if (a.bplog) {
+            if (nround > z.d.bpcap && !z.status) z.status = kErrBpLog;
+            if (lane == 0) a.bplog[z.d.bp_off] = nround;
         }
     }
     dp_helper_exit(z);

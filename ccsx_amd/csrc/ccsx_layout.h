@@ -66,6 +66,7 @@ enum Status : int32_t {
     kErrReadLen = 6,   // pushed read longer than the LDS read buffer (re-run with an uncapped buffer)
     kErrOut = 7,       // CCS longer than the output slab
     kErrTrace = 8,     // traceback did not terminate (internal error)
+    kErrBpLog = 9,     // more shredding rounds than the breakpoint log holds (re-run with full caps)
 };
 
 enum Mode : int32_t { kShred = 0, kPrimitive = 1, kSinglePoa = 2 };
@@ -81,6 +82,9 @@ struct ZmwDesc {
     uint32_t wcap;      // rows of wide slot records (rcap if n > 64, else 0)
     uint32_t outcap;    // output slab capacity (bytes)
     uint32_t msacap;    // MSA slab capacity (bytes)
+    uint64_t bp_off;    // breakpoint log (-v >= 3): word offset of {rounds, (i, ncols) x bpcap}
+    uint32_t bpcap;     // rounds the log holds (0: no log)
+    uint32_t pad_;
 };
 
 struct ZLayout {
@@ -220,6 +224,7 @@ struct KArgs {
     uint32_t lds_read_words;    // 0: the HBM-read kernel instance (read and cursors in the workspace)
     uint32_t lds_nmax;
     unsigned long long *prof;  // optional: kProfSlots shader-clock counters per ZMW (diagnostics)
+    uint32_t *bplog;           // optional: per-round breakpoint log (main.c:619-620, ZmwDesc::bp_off)
 };
 
 // phase counters written when KArgs::prof != nullptr

@@ -48,6 +48,7 @@ struct Zmw {
     std::vector<uint8_t> seg_rev;
     std::string ccs;
     int32_t status = 0;
+    std::vector<uint32_t> bp;  // -v >= 3: (breakpoint, MSA columns) per shredding round
 };
 
 struct Chunk {
@@ -354,6 +355,7 @@ int main(int argc, char **argv)
         if (ccsx_gpu_open(dev, &ctx[i]) != 0) return 1;
         ccsx_gpu_set_mem_share(ctx[i], (uint32_t)per_dev[dev]);
         ccsx_gpu_set_prealloc(ctx[i], 1);
+        if (verbose > 2 && split_subread) ccsx_gpu_set_bp_log(ctx[i], 1);
     }
 
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
@@ -394,6 +396,10 @@ int main(int argc, char **argv)
                         Zmw &z = ch.zs[b.idx[i]];
                         z.status = out[i].status;
                         if (!out[i].status) z.ccs.assign(out[i].ccs, out[i].len);
+                        const uint32_t *lg;
+                        uint32_t nr = 0;
+                        if (verbose > 2 && !out[i].status && ccsx_gpu_bp_log(ctx[w], i, &lg, &nr) == 0)
+                            z.bp.assign(lg, lg + 2 * (size_t)nr);
                     }
                 } else {
                     std::lock_guard<std::mutex> g(err_m);
@@ -416,6 +422,14 @@ int main(int argc, char **argv)
     size_t nfail = 0;
     std::thread writer([&]() {
         while (auto ch = ring.next_done()) {
+            if (!fatal && verbose > 2) {
+                // main.c:619-620, printed by ccs_for2 during step 1 (so before
+                // the chunk's records), to stdout
+                for (auto &z : ch->zs)
+                    for (size_t r = 0; r + 1 < z.bp.size(); r += 2)
+                        fprintf(stdout, "breakpoint=%u maplen=%u nseq=%zu hole=%s\n", z.bp[r], z.bp[r + 1],
+                                z.seg_len.size(), z.hole.c_str());
+            }
             if (!fatal) {
                 for (auto &z : ch->zs) {
                     if (z.status) {

@@ -25,7 +25,8 @@ EXPORTS = {
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
                    "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows",
                    "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault",
-                   "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count"],
+                   "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count",
+                   "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
                     "ccsx_zmw_cost", "ccsx_partition",

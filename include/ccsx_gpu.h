@@ -77,6 +77,13 @@ int ccsx_gpu_set_mem_share(ccsx_ctx *ctx, uint32_t share);
  * not).  For long runs such as the CLI's growing chunks. */
 int ccsx_gpu_set_prealloc(ccsx_ctx *ctx, int on);
 
+/* -v >= 3 (main.c:619-620): on != 0 makes the following ccsx_gpu_run calls
+ * (shredded mode) record, per ZMW and shredding round, the breakpoint i and
+ * the MSA's column count (msaidxs->size) that ccs_for2 prints.
+ * ccsx_gpu_bp_log: the log of ZMW `zmw` (index into the last ccsx_gpu_run's
+ * batch) as nrounds (i, ncols) pairs, ctx-owned until the next run. */
+int ccsx_gpu_set_bp_log(ccsx_ctx *ctx, int on);
+int ccsx_gpu_bp_log(const ccsx_ctx *ctx, size_t zmw, const uint32_t **pairs, uint32_t *nrounds);
 /* The same in three steps (one slice, tight capacities, no re-run), so inputs
  * can stay resident in HBM across launches (used by bench.py).
  * ccsx_gpu_launch returns the kernel time measured with HIP events on the

@@ -48,6 +48,9 @@ def lib() -> C.CDLL:
                                      C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.POINTER(C.c_uint32)),
                                      C.POINTER(C.c_uint32), C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
                                      C.POINTER(C.c_uint64)]
+        L.ocsx_zmw_log.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                   C.c_uint32, C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.ocsx_zmw_log.restype = C.c_size_t
         L.ocsx_edit_distance.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32]
         L.ocsx_edit_distance.restype = C.c_int64
         _lib = L
@@ -104,6 +107,19 @@ class Poa:
         n = self._L.ocsx_zmw(self._g, mode, seqs, offs.ctypes.data_as(C.POINTER(C.c_uint32)),
                              lens.ctypes.data_as(C.POINTER(C.c_uint32)), len(lens), out)
         return out.raw[:n]
+
+    def zmw_breakpoints(self, seqs: bytes, offs, lens) -> tuple[bytes, list[tuple[int, int]]]:
+        """ccs_for2 plus, per shredding round, (breakpoint, MSA columns): the
+        values main.c:619-620 prints at -v >= 3."""
+        offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = C.create_string_buffer(int(lens.sum()) + 16)
+        cap = int(lens.sum()) + 2
+        log = (C.c_uint32 * (2 * cap))()
+        nbp = C.c_uint32(0)
+        n = self._L.ocsx_zmw_log(self._g, 0, seqs, offs.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                 lens.ctypes.data_as(C.POINTER(C.c_uint32)), len(lens), out, log, cap, C.byref(nbp))
+        return out.raw[:n], [(log[2 * i], log[2 * i + 1]) for i in range(nbp.value)]
 
     def cells(self) -> int:
         return int(self._L.opoa_cells(self._g))

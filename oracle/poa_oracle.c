@@ -570,10 +570,21 @@ uint32_t opoa_nrows(const opoa_t *g) { return g->g.R; }
 
 static const char BIT_BASE[5] = {'A', 'C', 'G', 'T', 'N'};
 
-/* ccs_for (main.c:455-508) and ccs_for2 (main.c:510-647) after ccs_prepare. */
+/* ccs_for (main.c:455-508) and ccs_for2 (main.c:510-647) after ccs_prepare.
+ * bplog (optional, shredded mode): per round the pair (breakpoint i,
+ * msaidxs->size) that main.c:619-620 prints at -v >= 3, at most bpcap pairs;
+ * *nbp = the number of rounds. */
 size_t ocsx_zmw(opoa_t *g, int mode, const char *seqs, const uint32_t *offs,
                 const uint32_t *lens, uint32_t n, char *out)
 {
+    return ocsx_zmw_log(g, mode, seqs, offs, lens, n, out, NULL, 0, NULL);
+}
+
+size_t ocsx_zmw_log(opoa_t *g, int mode, const char *seqs, const uint32_t *offs, const uint32_t *lens, uint32_t n,
+                    char *out, uint32_t *bplog, uint32_t bpcap, uint32_t *nbp)
+{
+    uint32_t nround = 0;
+    if (nbp) *nbp = 0;
     size_t ol = 0;
     if (mode == 1) {
         opoa_beg(g);
@@ -633,6 +644,9 @@ size_t ocsx_zmw(opoa_t *g, int mode, const char *seqs, const uint32_t *offs,
             }
             if (i >= 1) break;
         }
+        /* main.c:619-620 (-v >= 3) */
+        if (bplog && nround < bpcap) bplog[2 * nround] = i, bplog[2 * nround + 1] = g->ncols;
+        ++nround;
         /* main.c:622-638 */
         for (uint32_t j = 0; j < i; j++) {
             const uint8_t *col = g->msacols + (size_t)g->msaidxs[j] * mrow;
@@ -645,6 +659,7 @@ size_t ocsx_zmw(opoa_t *g, int mode, const char *seqs, const uint32_t *offs,
     free(pos);
     free(rowcnt);
     out[ol] = 0;
+    if (nbp) *nbp = nround;
     return ol;
 }
 

@@ -43,6 +43,10 @@ uint32_t opoa_nrows(const opoa_t *g);   /* graph nodes after opoa_end */
  * Writes the ASCII CCS into out (capacity >= sum(lens)); returns its length. */
 size_t ocsx_zmw(opoa_t *g, int mode, const char *seqs, const uint32_t *offs,
                 const uint32_t *lens, uint32_t n, char *out);
+/* The same, recording per shredding round (breakpoint, MSA columns) -- the
+ * values main.c:619-620 prints at -v >= 3 -- into bplog (bpcap pairs). */
+size_t ocsx_zmw_log(opoa_t *g, int mode, const char *seqs, const uint32_t *offs, const uint32_t *lens, uint32_t n,
+                    char *out, uint32_t *bplog, uint32_t bpcap, uint32_t *nbp);
 
 /* Many ZMWs on nthreads CPU threads (kt_for semantics); out[i] capacity
  * >= sum(lens[i]) + 1; cells[i] = DP cells of ZMW i. */

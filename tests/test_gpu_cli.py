@@ -133,3 +133,23 @@ def test_cli_repeated_exclude(tmp_path, xargs, excluded):
     got = open(out, "rb").read()
     assert got == _expected(fa, 0, exclude=excluded)
     assert got.count(b">") == 40 - len(excluded)
+
+
+def test_cli_breakpoint_lines(tmp_path):
+    """-v -v -v prints ccs_for2's per-round breakpoint line to stdout
+    (main.c:619-620: breakpoint, MSA columns, nseq, hole) for every shredding
+    round, the final one included (breakpoint = columns); the values are the
+    oracle's rounds for the same push lists, in input order."""
+    from oracle.oracle import Poa
+    fa = str(tmp_path / "in.fa")
+    write(fa, 6, 7000, 6)
+    out = str(tmp_path / "out.fa")
+    r = _run(["-A", "-v", "-v", "-v", "-j", "2", fa, out])
+    got = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("breakpoint=")]
+    want = []
+    for movie, hole, subs in cx.read_zmws(fa, False):
+        p = cx.prepare(subs)
+        _, bps = Poa().zmw_breakpoints(p.seqs, p.offs, p.lens)
+        want += [f"breakpoint={i} maplen={c} nseq={len(p.lens)} hole={hole}" for i, c in bps]
+    assert len(want) > 12 and got == want
+    assert open(out, "rb").read() == _expected(fa, 0)

@@ -3,7 +3,7 @@
 # timing (tools/gpu_ab.sh).  The flags go to every kernel configuration
 # (after its own defines, so they override them) and to the host launcher;
 # the configurations' defines come from ccsx_amd/build.py (KCFGS).
-#   [CFGS="tput occ"] tools/build_variant.sh TAG -DFOO=1 ...
+#   [CFGS="tput occ"] [KSRC=path/to/kernel.hip] tools/build_variant.sh TAG -DFOO=1 ...
 # CFGS limits the extra flags to the named configurations (default: all).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -17,7 +17,7 @@ while read -r NAME DEFS; do
   X=("$@")
   [ -n "$CFGS" ] && [[ " $CFGS " != *" $NAME "* ]] && X=()
   rm -f $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o
-  $K $DEFS "${X[@]}" -c $C/ccsx_kernel.hip -o $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o &
+  $K $DEFS "${X[@]}" -c ${KSRC:-$C/ccsx_kernel.hip} -o $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o &
   KOBJS="$KOBJS $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o"
 done < <(cd "$ROOT" && python3 -c "from ccsx_amd.build import KCFGS; [print(n, ' '.join(d)) for n, d in KCFGS]")
 /opt/rocm/bin/hipcc -x c++ -O3 -std=c++17 -fPIC $INC -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include "$@" \

@@ -9,7 +9,7 @@
 #   parity             tests/test_gpu_parity.py only
 #   bench              the default bench.py line (config B, 20 steps, e2e, cpu baseline)
 #   bench:CFG[:KCFG]   bench.py --config CFG (B|C|D|E|H), 3 steps, optional forced kernel cfg
-#   ab:CFG:KCFG,...    interleaved rounds of bench --config CFG over several kernel cfgs
+#   ab:CFG:KCFG,...[:LIB,...]  3 interleaved rounds of bench --config CFG over kernel cfgs x libraries
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
@@ -31,8 +31,8 @@ bench_args() {  # CFG [KCFG]
 }
 
 step() {
-  local s=$1 name cfg k
-  IFS=: read -r name cfg k <<< "$s"
+  local s=$1 name cfg k x
+  IFS=: read -r name cfg k x <<< "$s"
   case $name in
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gputest.log" 2>&1
@@ -48,13 +48,17 @@ step() {
       local f="$OUT/bench_${cfg}${k:+_k$k}${CCSX_LIB:+_${CCSX_LIB%.so}}.json"
       timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$k") > "$f" 2> "${f%.json}.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['value'], 'ZMWs/s', d['gcups'], 'GCUPS', 'cfg', d['roofline'].get('kernel_cfg'))" "$f" ;;
-    ab)
-      local i kk f
+    ab)  # ab:CFG:KCFG[,KCFG...][:LIB,LIB...] -- 3 interleaved rounds over kernel cfgs x libraries
+      local i kk f L libs
+      libs=${libs_ab:-libccsx_amd.so}
+      [ -n "$x" ] && libs=$x
       for i in 1 2 3; do
-        for kk in ${k//,/ }; do
-          f="$OUT/ab_${cfg}_k${kk}_$i.json"
-          timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$kk") > "$f" 2> "${f%.json}.err" || return 1
-          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['gcups'], 'GCUPS')" "$f"
+        for L in ${libs//,/ }; do
+          for kk in ${k//,/ }; do
+            f="$OUT/ab_${cfg}_k${kk}_${L%.so}_$i.json"
+            CCSX_LIB=$L timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$kk") > "$f" 2> "${f%.json}.err" || return 1
+            python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'k', sys.argv[3], d['ms_per_step'], 'ms', d['gcups'], 'GCUPS')" "$f" "$L" "$kk"
+          done
         done
       done ;;
     kt)
