@@ -2,7 +2,8 @@
 //
 // Stages a chunk of ZMWs into HBM (one sequence arena, segment tables, one
 // descriptor and one workspace slab per ZMW, laid out by ccsx_layout.h),
-// launches one 64-lane workgroup per ZMW and copies the CCS strings back.
+// launches one workgroup per ZMW and copies the CCS strings back; slices of
+// a large chunk alternate between two slots (streams) so they overlap.
 // This is the device boundary that replaces kt_for(ccs_for2/ccs_for) in step 1
 // of ccsx's pipeline (main.c:698-706).
 #include "ccsx_gpu.h"
@@ -135,23 +136,52 @@ struct DevBuf {
     }
 };
 
+
+// One staged slice and everything it owns on the device and the host.  A
+// context has two: ccsx_gpu_run stages and launches slice k + 1 on the other
+// slot's stream while slice k's kernel runs, so one slice's tail (the launch
+// ends with its slowest ZMW) overlaps the next slice's start, and its staging
+// overlaps the previous kernel.  stage / launch / fetch (bench.py) use slot 0.
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    size_t nz = 0;
+    uint32_t lds_read_words = 0, lds_nmax = 0;
+    int32_t cfg = ccsx::kCfgLatency;   // kernel configuration of the staged slice
+    uint64_t seq_bytes = 0, ws_bytes = 0, out_bytes = 0, msa_bytes = 0, bp_words = 0;
+    uint32_t nseg_total = 0;
+    bool inflight = false;             // launched, results not fetched yet
+    std::vector<ccsx::ZmwDesc> desc;
+    std::vector<uint32_t> hoff, hlen, order;  // host copies the async H2D reads from
+    DevBuf d_prof, d_bp;
+    DevBuf d_seq, d_soff, d_slen, d_desc, d_order, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
+    HostBuf h_out, h_seq;
+    std::vector<uint32_t> h_olen, h_ncols, h_bp;
+    std::vector<int32_t> h_status;
+    std::vector<unsigned long long> h_cells, h_prof;
+    std::vector<uint8_t> h_msa;
+    void release()
+    {
+        DevBuf *bufs[] = {&d_bp, &d_prof, &d_seq, &d_soff, &d_slen, &d_desc, &d_order, &d_ws, &d_out,
+                          &d_msa, &d_olen, &d_ncols, &d_status, &d_cells};
+        for (DevBuf *b : bufs) b->release();
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+        ev0 = ev1 = nullptr;
+        stream = nullptr;
+    }
+};
+
 }  // namespace
 
 struct ccsx_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
-    // staged batch
-    size_t nz = 0;
-    uint32_t lds_read_words = 0, lds_nmax = 0;
-    int32_t cfg = ccsx::kCfgLatency;   // kernel configuration of the staged slice
+    Slot slot[2];
     int32_t cfg_force = -1;            // test hook: -1 = by slice size
     uint32_t ncu = 256;                // compute units of the device
     uint64_t reruns = 0;               // ZMWs ccsx_gpu_run re-ran with full caps
-    uint64_t seq_bytes = 0, ws_bytes = 0, out_bytes = 0, msa_bytes = 0;
-    uint32_t nseg_total = 0;
-    std::vector<ccsx::ZmwDesc> desc;
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
     int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
@@ -159,22 +189,10 @@ struct ccsx_ctx {
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
     bool prealloc = false;             // reserve the slice budget up front
     bool bp_log = false;               // record the -v >= 3 breakpoint log (main.c:619-620)
-    uint64_t bp_words = 0;             // words of the staged slice's breakpoint log
-    DevBuf d_bp;
-    std::vector<uint32_t> h_bp;
     std::vector<uint32_t> run_bp;      // ccsx_gpu_run: the gathered logs, (i, ncols) pairs
     std::vector<uint64_t> run_bp_off;  // per ZMW of the call: offset into run_bp (pairs)
     std::vector<uint32_t> run_bp_n;    // per ZMW of the call: rounds
     std::vector<uint8_t> run_arena;    // ccsx_gpu_run's gathered CCS strings
-    DevBuf d_prof;
-    std::vector<unsigned long long> h_prof;
-    DevBuf d_seq, d_soff, d_slen, d_desc, d_order, d_ws, d_out, d_msa, d_olen, d_ncols, d_status, d_cells;
-    // fetched results
-    HostBuf h_out, h_seq;
-    std::vector<uint32_t> h_olen, h_ncols;
-    std::vector<int32_t> h_status;
-    std::vector<unsigned long long> h_cells;
-    std::vector<uint8_t> h_msa;
 };
 
 static int fail(ccsx_ctx *c, const char *what, hipError_t e)
@@ -206,9 +224,11 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
     auto *c = new ccsx_ctx();
     c->device = device;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
-    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    for (Slot &s : c->slot) {
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreate(&s.ev0);
+        if (e == hipSuccess) e = hipEventCreate(&s.ev1);
+    }
     if (e == hipSuccess) {
         int n = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0)
@@ -216,6 +236,7 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
     }
     if (e != hipSuccess) {
         fprintf(stderr, "[ccsx_gpu] cannot open device %d: %s\n", device, hipGetErrorString(e));
+        for (Slot &s : c->slot) s.release();
         delete c;
         return -1;
     }
@@ -227,12 +248,10 @@ void ccsx_gpu_close(ccsx_ctx *c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    DevBuf *bufs[] = {&c->d_bp, &c->d_prof, &c->d_seq, &c->d_soff, &c->d_slen, &c->d_desc, &c->d_order, &c->d_ws, &c->d_out,
-                      &c->d_msa, &c->d_olen, &c->d_ncols, &c->d_status, &c->d_cells};
-    for (DevBuf *b : bufs) b->release();
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (Slot &s : c->slot) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        s.release();
+    }
     delete c;
 }
 
@@ -255,9 +274,13 @@ const char *ccsx_gpu_status_str(int32_t s)
     }
 }
 
-// pinned staging arenas of a preallocating context: big enough for a batch
-// of ~10k config-E ZMWs (1.3 GB of subreads) without re-pinning
-constexpr size_t kPinnedFloor = 2ull << 30;
+}  // extern "C"
+
+// pinned staging arenas of a preallocating context (per slot): the subreads
+// and CCS of a CLI micro-batch (a 16,384-ZMW config-E chunk over one
+// context's two batches: ~1 GB of subreads) without re-pinning; grown on
+// demand beyond it.  INTEGRATION.md lists the host-memory footprint.
+constexpr size_t kPinnedSeqFloor = 512ull << 20, kPinnedOutFloor = 128ull << 20;
 
 // LDS read buffer limits of the LDS kernel instance: reads up to 100 kb
 // (50 KiB of nibble pairs, 2 workgroups per CU) and 4,096 segments; beyond
@@ -300,14 +323,17 @@ static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, uint32_t tight_rows,
     return ccsx::align256(L.total) + hi + d.outcap + uint64_t(zi.nseg) * 8 + sizeof(ccsx::ZmwDesc) + 32;
 }
 
-// internal: stage with an optional MSA slab per ZMW (single-POA mode) and
-// full (exact upper bound) or tight capacities (ccsx_layout.h:zcaps)
-int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa, int full_caps)
+// Stage a slice into slot s: sizes, device buffers, the host packing of the
+// sequence arena, and the H2D copies enqueued on the slot's stream (the host
+// copies they read stay in the slot until its next stage, which follows the
+// slot's fetch, i.e. a stream synchronisation).  with_msa: an MSA slab per
+// ZMW (single-POA mode); full_caps: exact upper-bound capacities, else tight
+// ones (ccsx_layout.h zcaps).
+static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int with_msa, int full_caps)
 {
-    if (!c) return -1;
     HIPCHK(c, hipSetDevice(c->device));
-    c->nz = nz;
-    c->desc.assign(nz, ccsx::ZmwDesc{});
+    s.nz = nz;
+    s.desc.assign(nz, ccsx::ZmwDesc{});
     uint64_t seq_b = 0, ws_b = 0, out_b = 0, msa_b = 0, bp_w = 0;
     uint32_t nseg = 0, lmax_all = 0, nmax = 0;
     for (size_t i = 0; i < nz; ++i) {
@@ -319,7 +345,7 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
             c->err = "ZMW too large (sum of segment lengths >= 2^30)";
             return -1;
         }
-        ccsx::ZmwDesc &d = c->desc[i];
+        ccsx::ZmwDesc &d = s.desc[i];
         ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows, c->shred_caps);
         d.seg0 = nseg;
         d.seq_off = seq_b;
@@ -343,16 +369,16 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
         lmax_all = std::max(lmax_all, lmax);
         nmax = std::max(nmax, zi.nseg);
     }
-    c->seq_bytes = seq_b, c->ws_bytes = ws_b, c->out_bytes = out_b, c->msa_bytes = msa_b;
-    c->bp_words = bp_w;
-    c->nseg_total = nseg;
+    s.seq_bytes = seq_b, s.ws_bytes = ws_b, s.out_bytes = out_b, s.msa_bytes = msa_b;
+    s.bp_words = bp_w;
+    s.nseg_total = nseg;
     // nibble-pair read buffer (ccsx_kernel.hip load_read); at least one band:
     // every lane reads its window bytes even when the read is shorter.  A
     // slice with a read or a cursor array beyond the LDS budget runs the
     // HBM-read kernel instance (lds_read_words = 0)
     if (lmax_all > kLdsReadMaxBases || nmax > kLdsMaxSegs) {
-        c->lds_read_words = 0;
-        c->lds_nmax = 0;
+        s.lds_read_words = 0;
+        s.lds_nmax = 0;
     } else {
         // shredded mode pushes windows of ~2-5 kb, not whole segments: with
         // tight caps the buffer is capped at kShredReadCap bases (a longer
@@ -361,21 +387,21 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
         // one more workgroup per CU
         uint32_t lb = std::max<uint32_t>(lmax_all, ccsx::kW);
         if (c->shred_caps && !full_caps) lb = std::min(lb, kShredReadCap);
-        c->lds_read_words = (lb + 7) / 8 + 2;
-        c->lds_nmax = std::max<uint32_t>(nmax, 1);
+        s.lds_read_words = (lb + 7) / 8 + 2;
+        s.lds_nmax = std::max<uint32_t>(nmax, 1);
     }
     // kernel configuration: the latency one if it keeps the whole slice
     // resident, else the occupancy one (ccsx_layout.h KernelCfg)
     {
-        const uint32_t extra = c->lds_read_words + c->lds_nmax;
+        const uint32_t extra = s.lds_read_words + s.lds_nmax;
         const size_t res_lat = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgLatency, extra);
-        c->cfg = c->cfg_force >= 0 ? c->cfg_force : (nz <= res_lat ? ccsx::kCfgLatency : ccsx::kCfgOccupancy);
+        s.cfg = c->cfg_force >= 0 ? c->cfg_force : (nz <= res_lat ? ccsx::kCfgLatency : ccsx::kCfgOccupancy);
     }
     size_t freeb = 0, totb = 0;
     const auto ti = std::chrono::steady_clock::now();
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
-    const uint64_t need = seq_b + ws_b + out_b + msa_b + uint64_t(nseg) * 8 + nz * (sizeof(ccsx::ZmwDesc) + 32);
-    if (need + (1ull << 30) > freeb + c->d_ws.cap + c->d_seq.cap + c->d_out.cap + c->d_msa.cap) {
+    const uint64_t need = seq_b + ws_b + out_b + msa_b + bp_w * 4 + uint64_t(nseg) * 8 + nz * (sizeof(ccsx::ZmwDesc) + 32);
+    if (need + (1ull << 30) > freeb + s.d_ws.cap + s.d_seq.cap + s.d_out.cap + s.d_msa.cap) {
         char m[160];
         snprintf(m, sizeof m, "batch needs %.1f GB of device memory, %.1f GB free: use a smaller chunk",
                  need / 1e9, freeb / 1e9);
@@ -385,55 +411,147 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     using tms = std::chrono::duration<double, std::milli>;
     const auto ta = std::chrono::steady_clock::now();
-    HIPCHK(c, c->d_seq.reserve(seq_b));
-    HIPCHK(c, c->d_soff.reserve(size_t(nseg) * 4));
-    HIPCHK(c, c->d_slen.reserve(size_t(nseg) * 4));
-    HIPCHK(c, c->d_desc.reserve(nz * sizeof(ccsx::ZmwDesc)));
-    HIPCHK(c, c->d_order.reserve(nz * 4));
-    HIPCHK(c, c->d_ws.reserve(ws_b));
-    HIPCHK(c, c->d_out.reserve(out_b));
-    HIPCHK(c, c->d_msa.reserve(msa_b));
-    HIPCHK(c, c->d_olen.reserve(nz * 4));
-    HIPCHK(c, c->d_ncols.reserve(nz * 4));
-    HIPCHK(c, c->d_status.reserve(nz * 4));
-    HIPCHK(c, c->d_cells.reserve(nz * 8));
-    if (bp_w) HIPCHK(c, c->d_bp.reserve(bp_w * 4));
+    HIPCHK(c, s.d_seq.reserve(seq_b));
+    HIPCHK(c, s.d_soff.reserve(size_t(nseg) * 4));
+    HIPCHK(c, s.d_slen.reserve(size_t(nseg) * 4));
+    HIPCHK(c, s.d_desc.reserve(nz * sizeof(ccsx::ZmwDesc)));
+    HIPCHK(c, s.d_order.reserve(nz * 4));
+    HIPCHK(c, s.d_ws.reserve(ws_b));
+    HIPCHK(c, s.d_out.reserve(out_b));
+    HIPCHK(c, s.d_msa.reserve(msa_b));
+    HIPCHK(c, s.d_olen.reserve(nz * 4));
+    HIPCHK(c, s.d_ncols.reserve(nz * 4));
+    HIPCHK(c, s.d_status.reserve(nz * 4));
+    HIPCHK(c, s.d_cells.reserve(nz * 8));
+    if (bp_w) HIPCHK(c, s.d_bp.reserve(bp_w * 4));
     const auto tb = std::chrono::steady_clock::now();
     // host staging of the sequence arena and segment tables
-    HIPCHK(c, c->h_seq.reserve(seq_b, c->prealloc ? kPinnedFloor : 0));
-    uint8_t *hseq = c->h_seq.p;
-    std::vector<uint32_t> hoff(nseg), hlen(nseg);
+    HIPCHK(c, s.h_seq.reserve(seq_b, c->prealloc ? kPinnedSeqFloor / c->mem_share : 0));
+    uint8_t *hseq = s.h_seq.p;
+    s.hoff.resize(nseg);
+    s.hlen.resize(nseg);
     for (size_t i = 0; i < nz; ++i) {
         const ccsx_zmw_in &zi = z[i];
-        const ccsx::ZmwDesc &d = c->desc[i];
+        const ccsx::ZmwDesc &d = s.desc[i];
         uint64_t hi = 0;
         for (uint32_t k = 0; k < zi.nseg; ++k) {
-            hoff[d.seg0 + k] = zi.seg_off[k];
-            hlen[d.seg0 + k] = zi.seg_len[k];
+            s.hoff[d.seg0 + k] = zi.seg_off[k];
+            s.hlen[d.seg0 + k] = zi.seg_len[k];
             hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
         }
         if (hi) memcpy(hseq + d.seq_off, zi.seqs, hi);
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_seq.p, hseq, seq_b, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_soff.p, hoff.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_slen.p, hlen.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_desc.p, c->desc.data(), nz * sizeof(ccsx::ZmwDesc), hipMemcpyHostToDevice,
-                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(s.d_seq.p, hseq, seq_b, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(c, hipMemcpyAsync(s.d_soff.p, s.hoff.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(c, hipMemcpyAsync(s.d_slen.p, s.hlen.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(c, hipMemcpyAsync(s.d_desc.p, s.desc.data(), nz * sizeof(ccsx::ZmwDesc), hipMemcpyHostToDevice, s.stream));
     // launch order: decreasing estimated POA work (ccsx_zmw_cost: S x (28 +
     // n)), ties in input order -- longest-processing-time first, so a launch
-    // ends on its cheapest ZMWs.  (Round 1 ordered by rcap, which the tight
-    // shredded caps clamp to one value for every segment above 8 kb: config-E
-    // slices launched in input order.)
-    std::vector<uint32_t> order(nz);
+    // ends on its cheapest ZMWs
+    s.order.resize(nz);
     std::vector<uint64_t> cost(nz);
-    for (size_t i = 0; i < nz; ++i) order[i] = uint32_t(i), cost[i] = ccsx_zmw_cost(z[i].seg_len, z[i].nseg);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
-    HIPCHK(c, hipMemcpyAsync(c->d_order.p, order.data(), nz * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < nz; ++i) s.order[i] = uint32_t(i), cost[i] = ccsx_zmw_cost(z[i].seg_len, z[i].nseg);
+    std::stable_sort(s.order.begin(), s.order.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
+    HIPCHK(c, hipMemcpyAsync(s.d_order.p, s.order.data(), nz * 4, hipMemcpyHostToDevice, s.stream));
     if (timing)
-        fprintf(stderr, "[ccsx_gpu_stage] %zu ZMWs: meminfo %.0f ms, reserve %.0f ms (ws cap %.1f GB), pack+copy %.1f MB %.0f ms\n",
-                nz, tms(ta - ti).count(), tms(tb - ta).count(), c->d_ws.cap / 1e9, seq_b / 1e6,
+        fprintf(stderr, "[ccsx_gpu_stage] %zu ZMWs: meminfo %.0f ms, reserve %.0f ms (ws cap %.1f GB), pack %.1f MB %.0f ms\n",
+                nz, tms(ta - ti).count(), tms(tb - ta).count(), s.d_ws.cap / 1e9, seq_b / 1e6,
                 tms(std::chrono::steady_clock::now() - tb).count());
+    return 0;
+}
+
+// Enqueue the slot's kernel between its two events (asynchronous)
+static int launch_slot(ccsx_ctx *c, Slot &s, int mode)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    ccsx::KArgs a{};
+    a.seq = s.d_seq.as<uint8_t>();
+    a.soff = s.d_soff.as<uint32_t>();
+    a.slen = s.d_slen.as<uint32_t>();
+    a.desc = s.d_desc.as<ccsx::ZmwDesc>();
+    a.order = s.d_order.as<uint32_t>();
+    a.ws = s.d_ws.as<uint8_t>();
+    a.out = s.d_out.as<uint8_t>();
+    a.msa = s.d_msa.as<uint8_t>();
+    a.out_len = s.d_olen.as<uint32_t>();
+    a.ncols = s.d_ncols.as<uint32_t>();
+    a.status = s.d_status.as<int32_t>();
+    a.cells = s.d_cells.as<unsigned long long>();
+    a.mode = mode;
+    a.nzmw = uint32_t(s.nz);
+    a.lds_read_words = s.lds_read_words;
+    a.lds_nmax = s.lds_nmax;
+    a.prof = nullptr;
+    a.bplog = s.bp_words ? s.d_bp.as<uint32_t>() : nullptr;
+    if (c->profiling) {
+        HIPCHK(c, s.d_prof.reserve(s.nz * ccsx::kProfSlots * 8));
+        a.prof = s.d_prof.as<unsigned long long>();
+    }
+    const uint32_t lds = kcfg_lds(s.cfg, s.lds_read_words + s.lds_nmax);
+    if (lds > 160 * 1024) {
+        c->err = "reads too long for the LDS read buffer";
+        return -1;
+    }
+    HIPCHK(c, hipEventRecord(s.ev0, s.stream));
+    HIPCHK(c, kLaunch[s.cfg](&a, lds, s.stream));
+    HIPCHK(c, hipEventRecord(s.ev1, s.stream));
+    s.inflight = true;
+    return 0;
+}
+
+// Copy the slot's results back (after its kernel: same stream) and wait for
+// them; out[i] for i < s.nz.  Returns 0, -2 (some ZMWs failed) or -1.
+static int fetch_slot(ccsx_ctx *c, Slot &s, ccsx_zmw_out *out)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t nz = s.nz;
+    HIPCHK(c, s.h_out.reserve(s.out_bytes, c->prealloc ? kPinnedOutFloor / c->mem_share : 0));
+    s.h_olen.resize(nz);
+    s.h_status.resize(nz);
+    s.h_cells.resize(nz);
+    s.h_bp.resize(s.bp_words);
+    if (nz) {
+        HIPCHK(c, hipMemcpyAsync(s.h_olen.data(), s.d_olen.p, nz * 4, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(c, hipMemcpyAsync(s.h_status.data(), s.d_status.p, nz * 4, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(c, hipMemcpyAsync(s.h_cells.data(), s.d_cells.p, nz * 8, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(c, hipMemcpyAsync(s.h_out.p, s.d_out.p, s.out_bytes, hipMemcpyDeviceToHost, s.stream));
+        if (s.bp_words)
+            HIPCHK(c, hipMemcpyAsync(s.h_bp.data(), s.d_bp.p, s.bp_words * 4, hipMemcpyDeviceToHost, s.stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(s.stream));
+    s.inflight = false;
+    int bad = 0;
+    for (size_t i = 0; i < nz; ++i) {
+        out[i].ccs = reinterpret_cast<const char *>(s.h_out.p + s.desc[i].out_off);
+        out[i].len = s.h_status[i] ? 0 : s.h_olen[i];
+        out[i].status = s.h_status[i];
+        out[i].cells = s.h_cells[i];
+        if (s.h_status[i] && !bad) {
+            bad = 1;
+            char m[200];
+            snprintf(m, sizeof m, "ZMW %zu of the batch failed on the device: %s", i,
+                     ccsx_gpu_status_str(s.h_status[i]));
+            c->err = m;
+        }
+    }
+    return bad ? -2 : 0;
+}
+
+extern "C" {
+
+// internal: stage with an optional MSA slab per ZMW (single-POA mode) and
+// full (exact upper bound) or tight capacities (ccsx_layout.h:zcaps); slot 0
+int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa, int full_caps)
+{
+    if (!c) return -1;
+    Slot &s = c->slot[0];
+    if (s.inflight) {  // launched, never fetched: its results are dropped
+        HIPCHK(c, hipStreamSynchronize(s.stream));
+        s.inflight = false;
+    }
+    const int r = stage_slot(c, s, z, nz, with_msa, full_caps);
+    if (r) return r;
+    HIPCHK(c, hipStreamSynchronize(s.stream));
     return 0;
 }
 
@@ -442,45 +560,16 @@ int ccsx_gpu_stage(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz) { return ccsx_g
 int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
 {
     if (!c) return -1;
-    HIPCHK(c, hipSetDevice(c->device));
-    if (c->nz == 0) {
+    Slot &s = c->slot[0];
+    if (s.nz == 0) {
         if (kernel_ms) *kernel_ms = 0.f;
         return 0;
     }
-    ccsx::KArgs a{};
-    a.seq = c->d_seq.as<uint8_t>();
-    a.soff = c->d_soff.as<uint32_t>();
-    a.slen = c->d_slen.as<uint32_t>();
-    a.desc = c->d_desc.as<ccsx::ZmwDesc>();
-    a.order = c->d_order.as<uint32_t>();
-    a.ws = c->d_ws.as<uint8_t>();
-    a.out = c->d_out.as<uint8_t>();
-    a.msa = c->d_msa.as<uint8_t>();
-    a.out_len = c->d_olen.as<uint32_t>();
-    a.ncols = c->d_ncols.as<uint32_t>();
-    a.status = c->d_status.as<int32_t>();
-    a.cells = c->d_cells.as<unsigned long long>();
-    a.mode = mode;
-    a.nzmw = uint32_t(c->nz);
-    a.lds_read_words = c->lds_read_words;
-    a.lds_nmax = c->lds_nmax;
-    a.prof = nullptr;
-    a.bplog = c->bp_words ? c->d_bp.as<uint32_t>() : nullptr;
-    if (c->profiling) {
-        HIPCHK(c, c->d_prof.reserve(c->nz * ccsx::kProfSlots * 8));
-        a.prof = c->d_prof.as<unsigned long long>();
-    }
-    const uint32_t lds = kcfg_lds(c->cfg, c->lds_read_words + c->lds_nmax);
-    if (lds > 160 * 1024) {
-        c->err = "reads too long for the LDS read buffer";
-        return -1;
-    }
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, kLaunch[c->cfg](&a, lds, c->stream));
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-    HIPCHK(c, hipEventSynchronize(c->ev1));
+    const int r = launch_slot(c, s, mode);
+    if (r) return r;
+    HIPCHK(c, hipEventSynchronize(s.ev1));
     float ms = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&ms, s.ev0, s.ev1));
     if (kernel_ms) *kernel_ms = ms;
     return 0;
 }
@@ -497,37 +586,7 @@ int ccsx_gpu_launch(ccsx_ctx *c, int mode, float *kernel_ms)
 int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
 {
     if (!c) return -1;
-    HIPCHK(c, hipSetDevice(c->device));
-    const size_t nz = c->nz;
-    HIPCHK(c, c->h_out.reserve(c->out_bytes, c->prealloc ? kPinnedFloor : 0));
-    c->h_olen.resize(nz);
-    c->h_status.resize(nz);
-    c->h_cells.resize(nz);
-    if (nz) {
-        HIPCHK(c, hipMemcpyAsync(c->h_olen.data(), c->d_olen.p, nz * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_status.data(), c->d_status.p, nz * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_cells.data(), c->d_cells.p, nz * 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_out.p, c->d_out.p, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
-        c->h_bp.resize(c->bp_words);
-        if (c->bp_words)
-            HIPCHK(c, hipMemcpyAsync(c->h_bp.data(), c->d_bp.p, c->bp_words * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-    }
-    int bad = 0;
-    for (size_t i = 0; i < nz; ++i) {
-        out[i].ccs = reinterpret_cast<const char *>(c->h_out.p + c->desc[i].out_off);
-        out[i].len = c->h_status[i] ? 0 : c->h_olen[i];
-        out[i].status = c->h_status[i];
-        out[i].cells = c->h_cells[i];
-        if (c->h_status[i] && !bad) {
-            bad = 1;
-            char m[200];
-            snprintf(m, sizeof m, "ZMW %zu of the batch failed on the device: %s", i,
-                     ccsx_gpu_status_str(c->h_status[i]));
-            c->err = m;
-        }
-    }
-    return bad ? -2 : 0;
+    return fetch_slot(c, c->slot[0], out);
 }
 
 // statuses of a tight-cap slice that the full-cap (uncapped read buffer) re-run clears
@@ -539,6 +598,9 @@ static bool is_cap_error(int32_t s)
 
 // One chunk.  The chunk is cut into slices that fit the device's free memory
 // (tight caps); a ZMW that outgrows a tight cap is re-run with full caps.
+// Slices alternate between the context's two slots: slice k + 1 is staged and
+// launched while slice k's kernel runs, and slice k's results are collected
+// when its slot is needed again (or at the end).
 int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out)
 {
     if (!c) return -1;
@@ -547,6 +609,11 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         return -1;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    for (Slot &s : c->slot)
+        if (s.inflight) {  // a stage/launch without fetch: drop its results
+            HIPCHK(c, hipStreamSynchronize(s.stream));
+            s.inflight = false;
+        }
     struct ShredCaps {  // the window-sized tight caps for this call only
         ccsx_ctx *c;
         ShredCaps(ccsx_ctx *x, bool on) : c(x) { c->shred_caps = on; }
@@ -554,10 +621,10 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     } shred_caps(c, mode == CCSX_MODE_SHRED);
     size_t freeb = 0, totb = 0;
     HIPCHK(c, hipMemGetInfo(&freeb, &totb));
-    // the workspace may grow into what is free plus what it already holds;
-    // the sequence / output arenas it would need beside it stay counted as
-    // used (they are re-reserved per slice, not released)
-    const uint64_t held = c->d_ws.cap;
+    // the workspaces may grow into what is free plus what they already hold;
+    // the sequence / output arenas they would need beside them stay counted
+    // as used (they are re-reserved per slice, not released)
+    const uint64_t held = c->slot[0].d_ws.cap + c->slot[1].d_ws.cap;
     uint64_t budget = freeb + held > (3ull << 30) ? freeb + held - (3ull << 30) : (1ull << 30);
     {
         // at most half the device per context (and a fixed share of it when
@@ -569,13 +636,20 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         const uint64_t part = totb / (2ull * c->mem_share);
         budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
     }
+    // two slots in flight: each holds half
+    const uint64_t slot_budget = std::max<uint64_t>(1ull << 29, budget / 2);
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
-    if (c->prealloc && c->d_ws.cap < budget) {
-        const auto t0 = std::chrono::steady_clock::now();
-        HIPCHK(c, c->d_ws.reserve(budget, true));
-        if (timing)
-            fprintf(stderr, "[ccsx_gpu_run] dev %d: workspace of %.1f GB reserved in %.0f ms\n", c->device, budget / 1e9,
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    using ms = std::chrono::duration<double, std::milli>;
+    const auto t_run = std::chrono::steady_clock::now();
+    if (c->prealloc) {
+        for (Slot &s : c->slot)
+            if (s.d_ws.cap < slot_budget) {
+                const auto t0 = std::chrono::steady_clock::now();
+                HIPCHK(c, s.d_ws.reserve(slot_budget, true));
+                if (timing)
+                    fprintf(stderr, "[ccsx_gpu_run] dev %d: workspace of %.1f GB reserved in %.0f ms\n", c->device,
+                            slot_budget / 1e9, ms(std::chrono::steady_clock::now() - t0).count());
+            }
     }
     c->run_arena.clear();
     c->run_bp.clear();
@@ -584,6 +658,58 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     std::vector<uint64_t> aoff(nz, 0);
     std::vector<int> cls(nz, 0);
     std::string first_err;
+    // results of the slice in slot s (input indices idx[b, b + s.nz))
+    struct Pending {
+        const std::vector<uint32_t> *idx = nullptr;
+        size_t b = 0;
+        std::vector<uint32_t> *retry = nullptr;
+        std::chrono::steady_clock::time_point t0;
+    } pend[2];
+    std::vector<ccsx_zmw_out> o;
+    auto collect = [&](int si) -> int {
+        Slot &s = c->slot[si];
+        if (!s.inflight) return 0;
+        o.assign(s.nz, ccsx_zmw_out{});
+        const int r = fetch_slot(c, s, o.data());
+        if (r && r != -2) return r;
+        if (timing) {
+            float kms = 0.f;
+            (void)hipEventElapsedTime(&kms, s.ev0, s.ev1);
+            fprintf(stderr, "[ccsx_gpu_run] dev %d slot %d: %zu ZMWs (cfg %d), kernel %.0f ms, staged..collected %.0f-%.0f ms\n",
+                    c->device, si, s.nz, s.cfg, kms, ms(pend[si].t0 - t_run).count(),
+                    ms(std::chrono::steady_clock::now() - t_run).count());
+        }
+        const Pending &p = pend[si];
+        for (size_t i = 0; i < s.nz; ++i) {
+            const uint32_t g = (*p.idx)[p.b + i];
+            out[g].cells = o[i].cells;
+            out[g].status = o[i].status;
+            out[g].len = 0;
+            if (o[i].status) {
+                if (p.retry && is_cap_error(o[i].status)) {
+                    p.retry->push_back(g);
+                } else if (first_err.empty()) {
+                    char m[200];
+                    snprintf(m, sizeof m, "ZMW %u of the batch failed on the device: %s", g,
+                             ccsx_gpu_status_str(o[i].status));
+                    first_err = m;
+                }
+                continue;
+            }
+            aoff[g] = c->run_arena.size();
+            out[g].len = o[i].len;
+            c->run_arena.insert(c->run_arena.end(), o[i].ccs, o[i].ccs + o[i].len);
+            if (s.bp_words && mode == CCSX_MODE_SHRED) {
+                const uint32_t *lg = s.h_bp.data() + s.desc[i].bp_off;
+                c->run_bp_off[g] = c->run_bp.size() / 2;
+                c->run_bp_n[g] = lg[0];
+                c->run_bp.insert(c->run_bp.end(), lg + 1, lg + 1 + 2 * uint64_t(lg[0]));
+            }
+        }
+        return 0;
+    };
+    int next_slot = 0;
+    std::vector<ccsx_zmw_in> sub;
     auto run_list = [&](const std::vector<uint32_t> &idx, bool full, std::vector<uint32_t> *retry) -> int {
         size_t b = 0;
         while (b < idx.size()) {
@@ -591,55 +717,30 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             size_t e = b;
             while (e < idx.size()) {
                 const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows, c->shred_caps);
-                if (e > b && (need + x > budget || cls[idx[e]] != cls[idx[b]])) break;
+                if (e > b && (need + x > slot_budget || cls[idx[e]] != cls[idx[b]])) break;
                 need += x;
                 ++e;
             }
-            std::vector<ccsx_zmw_in> sub(e - b);
+            const int si = next_slot;
+            next_slot ^= 1;
+            int r = collect(si);  // the slot's previous slice
+            if (r) return r;
+            sub.resize(e - b);
             for (size_t i = b; i < e; ++i) sub[i - b] = z[idx[i]];
-            const auto t0 = std::chrono::steady_clock::now();
-            int r = ccsx_gpu_stage_ex(c, sub.data(), sub.size(), 0, full ? 1 : 0);
+            pend[si].idx = &idx;
+            pend[si].b = b;
+            pend[si].retry = retry;
+            pend[si].t0 = std::chrono::steady_clock::now();
+            r = stage_slot(c, c->slot[si], sub.data(), sub.size(), 0, full ? 1 : 0);
             if (r) return r;
-            const auto t1 = std::chrono::steady_clock::now();
-            float kms = 0.f;
-            r = ccsx_gpu_launch_ex(c, mode, timing ? &kms : nullptr);
+            r = launch_slot(c, c->slot[si], mode);
             if (r) return r;
-            std::vector<ccsx_zmw_out> o(sub.size());
-            r = ccsx_gpu_fetch(c, o.data());
-            if (r && r != -2) return r;
-            if (timing) {
-                using ms = std::chrono::duration<double, std::milli>;
-                fprintf(stderr, "[ccsx_gpu_run] dev %d slice %zu ZMWs (%s caps, %.1f GB budget %.1f GB): stage %.0f ms, "
-                        "kernel %.0f ms, launch+fetch %.0f ms\n", c->device, sub.size(), full ? "full" : "tight",
-                        need / 1e9, budget / 1e9, ms(t1 - t0).count(), kms, ms(std::chrono::steady_clock::now() - t1).count());
-            }
-            for (size_t i = 0; i < sub.size(); ++i) {
-                const uint32_t g = idx[b + i];
-                out[g].cells = o[i].cells;
-                out[g].status = o[i].status;
-                out[g].len = 0;
-                if (o[i].status) {
-                    if (retry && is_cap_error(o[i].status)) {
-                        retry->push_back(g);
-                    } else if (first_err.empty()) {
-                        char m[200];
-                        snprintf(m, sizeof m, "ZMW %u of the batch failed on the device: %s", g,
-                                 ccsx_gpu_status_str(o[i].status));
-                        first_err = m;
-                    }
-                    continue;
-                }
-                aoff[g] = c->run_arena.size();
-                out[g].len = o[i].len;
-                c->run_arena.insert(c->run_arena.end(), o[i].ccs, o[i].ccs + o[i].len);
-                if (c->bp_words && mode == CCSX_MODE_SHRED) {
-                    const uint32_t *lg = c->h_bp.data() + c->desc[i].bp_off;
-                    c->run_bp_off[g] = c->run_bp.size() / 2;
-                    c->run_bp_n[g] = lg[0];
-                    c->run_bp.insert(c->run_bp.end(), lg + 1, lg + 1 + 2 * uint64_t(lg[0]));
-                }
-            }
             b = e;
+        }
+        // both slots' results before the list's vectors go away
+        for (int k = 0; k < 2; ++k) {
+            const int r = collect(next_slot ^ (k == 0 ? 1 : 0));
+            if (r) return r;
         }
         return 0;
     };
@@ -658,7 +759,11 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         c->reruns += retry.size();
         r = run_list(retry, true, nullptr);
     }
-    if (r) return r;
+    if (r) {
+        for (Slot &s : c->slot)
+            if (s.inflight) (void)hipStreamSynchronize(s.stream), s.inflight = false;
+        return r;
+    }
     if (c->fault >= 0 && (size_t)c->fault < nz) {
         out[c->fault].status = ccsx::kErrTrace;
         out[c->fault].len = 0;
@@ -687,7 +792,7 @@ int ccsx_gpu_set_kernel_cfg(ccsx_ctx *c, int cfg)
     return 0;
 }
 
-int ccsx_gpu_kernel_cfg(const ccsx_ctx *c) { return c ? c->cfg : -1; }
+int ccsx_gpu_kernel_cfg(const ccsx_ctx *c) { return c ? c->slot[0].cfg : -1; }
 
 int64_t ccsx_gpu_rerun_count(const ccsx_ctx *c) { return c ? (int64_t)c->reruns : -1; }
 
@@ -738,26 +843,30 @@ int ccsx_gpu_profile(ccsx_ctx *c, uint64_t *sums, uint32_t nslots)
 {
     if (!c || !c->profiling || nslots < (uint32_t)ccsx::kProfSlots) return -1;
     HIPCHK(c, hipSetDevice(c->device));
-    c->h_prof.assign(c->nz * ccsx::kProfSlots, 0);
-    if (c->nz)
-        HIPCHK(c, hipMemcpy(c->h_prof.data(), c->d_prof.p, c->nz * ccsx::kProfSlots * 8, hipMemcpyDeviceToHost));
+    Slot &s = c->slot[0];
+    s.h_prof.assign(s.nz * ccsx::kProfSlots, 0);
+    if (s.nz)
+        HIPCHK(c, hipMemcpy(s.h_prof.data(), s.d_prof.p, s.nz * ccsx::kProfSlots * 8, hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < nslots; ++i) sums[i] = 0;
-    for (size_t z = 0; z < c->nz; ++z)
-        for (int i = 0; i < ccsx::kProfSlots; ++i) sums[i] += c->h_prof[z * ccsx::kProfSlots + i];
+    for (size_t zi = 0; zi < s.nz; ++zi)
+        for (int i = 0; i < ccsx::kProfSlots; ++i) sums[i] += s.h_prof[zi * ccsx::kProfSlots + i];
     return 0;
 }
 
 int ccsx_gpu_profile_zmw(ccsx_ctx *c, uint64_t *out, uint32_t nzmw, uint32_t nslots)
 {
-    if (!c || !c->profiling || nslots < (uint32_t)ccsx::kProfSlots || nzmw < c->nz) return -1;
+    if (!c || !c->profiling || nslots < (uint32_t)ccsx::kProfSlots || nzmw < c->slot[0].nz) return -1;
     HIPCHK(c, hipSetDevice(c->device));
-    if (c->nz) HIPCHK(c, hipMemcpy(out, c->d_prof.p, c->nz * ccsx::kProfSlots * 8, hipMemcpyDeviceToHost));
+    const Slot &s = c->slot[0];
+    if (s.nz) HIPCHK(c, hipMemcpy(out, s.d_prof.p, s.nz * ccsx::kProfSlots * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 
 uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *c)
 {
-    return c ? c->seq_bytes + c->ws_bytes + c->out_bytes + c->msa_bytes : 0;
+    if (!c) return 0;
+    const Slot &s = c->slot[0];
+    return s.seq_bytes + s.ws_bytes + s.out_bytes + s.msa_bytes;
 }
 
 // single-POA path used by the bspoa-compatible API (bspoa_gpu.cpp)
@@ -771,15 +880,16 @@ int ccsx_gpu_single_poa(ccsx_ctx *c, const ccsx_zmw_in *z, const uint8_t **cns, 
     ccsx_zmw_out o;
     r = ccsx_gpu_fetch(c, &o);
     if (r) return r;
-    c->h_ncols.resize(1);
-    HIPCHK(c, hipMemcpy(c->h_ncols.data(), c->d_ncols.p, 4, hipMemcpyDeviceToHost));
-    const uint64_t mb = uint64_t(c->h_ncols[0]) * (z->nseg + 4);
-    c->h_msa.resize(mb + 1);
-    if (mb) HIPCHK(c, hipMemcpy(c->h_msa.data(), c->d_msa.p, mb, hipMemcpyDeviceToHost));
+    Slot &s = c->slot[0];
+    s.h_ncols.resize(1);
+    HIPCHK(c, hipMemcpy(s.h_ncols.data(), s.d_ncols.p, 4, hipMemcpyDeviceToHost));
+    const uint64_t mb = uint64_t(s.h_ncols[0]) * (z->nseg + 4);
+    s.h_msa.resize(mb + 1);
+    if (mb) HIPCHK(c, hipMemcpy(s.h_msa.data(), s.d_msa.p, mb, hipMemcpyDeviceToHost));
     *cns = reinterpret_cast<const uint8_t *>(o.ccs);
     *ncns = o.len;
-    *msa = c->h_msa.data();
-    *ncols = c->h_ncols[0];
+    *msa = s.h_msa.data();
+    *ncols = s.h_ncols[0];
     return 0;
 }
 

@@ -102,9 +102,10 @@ int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
 /* Test hook: tight row capacity override (0 = default 3 x longest segment + 4096). */
 int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
 /* Kernel configuration of the next slices: -1 (default) = by slice size (the
- * latency configuration -- 8-row DP blocks, 32-row LDS ring -- when it keeps
- * the whole slice resident, else the occupancy one -- 4-row blocks, 24-row
- * ring, one more workgroup per CU); 0 / 1 force one (tests, A/B).
+ * latency configuration -- three waves, 8-row DP blocks, 32-row LDS ring --
+ * when it keeps the whole slice resident, else the occupancy one -- 4-row
+ * blocks, 24-row ring, one more workgroup per CU); 0 / 1 / 2 force one (2:
+ * the throughput configuration, two-wave workgroups, up to 8 per CU).
  * ccsx_gpu_kernel_cfg: the configuration of the last staged slice. */
 int ccsx_gpu_set_kernel_cfg(ccsx_ctx *ctx, int cfg);
 int ccsx_gpu_kernel_cfg(const ccsx_ctx *ctx);
