@@ -87,6 +87,27 @@ def make_batch(cfg: dict, rank: int):
     return zs
 
 
+def cgroup_cpu_quota() -> int:
+    """CPUs granted by the cgroup (v2 cpu.max, v1 cfs quota), 0 if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return 0
+
+
 def cpu_baseline(threads: int | None = None, sample_j1: int = 60):
     """Config A (BASELINE.json configs[0]) end to end on the host's CPU cores:
     1,000 synthetic ZMWs (10 kb x 8 passes) as a subread FASTA through
@@ -94,10 +115,14 @@ def cpu_baseline(threads: int | None = None, sample_j1: int = 60):
     scalar POA, with ccsx's chunked pipeline and -j threads (kt_for dynamic
     sharing).  It stands in for `ccsx -A -j N`, unbuildable here (bsalign is
     not vendored): a scalar C restatement, not bsalign's SIMD code.
-    -j N = every CPU of the process's affinity mask (the reference's -j goes
-    straight to kt_for, main.c:794-795, kthread.c:48-65), uncapped; the line
-    records the affinity count beside nproc.  -j 1 runs on a `sample_j1`-ZMW
-    prefix for the per-core rate."""
+    -j N = the CPUs this process may use (the reference's -j goes straight
+    to kt_for, main.c:794-795, kthread.c:48-65): the affinity mask, bounded by
+    the cgroup CPU quota when one is set, else by OMP_NUM_THREADS when the
+    environment states the job's share that way (a GPU box's affinity mask
+    lists the whole machine while it grants the job 16 CPUs; -j 256 there
+    measured 101 ZMWs/s against 182 at -j 16, r03e).  The line records
+    affinity, quota, OMP_NUM_THREADS and nproc beside N.
+    -j 1 runs on a `sample_j1`-ZMW prefix for the per-core rate."""
     import subprocess
     import tempfile
     from tools.gen_synth import write
@@ -106,8 +131,12 @@ def cpu_baseline(threads: int | None = None, sample_j1: int = 60):
         from ccsx_amd.build import build_oracle
         build_oracle()
     affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    # without a cgroup quota, the job's CPU share as its environment states it
+    # (OMP_NUM_THREADS: a GPU box sets it to the CPUs it grants per GPU)
+    share = quota or int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if threads is None:
-        threads = max(1, affinity)
+        threads = max(1, min(affinity, share) if share else affinity)
     d = tempfile.mkdtemp(prefix="ccsx_cpu_")
     fa, fa1 = os.path.join(d, "a.fa"), os.path.join(d, "a1.fa")
     write(fa, 1000, 10000, 8, seed=SEED)
@@ -127,11 +156,13 @@ def cpu_baseline(threads: int | None = None, sample_j1: int = 60):
         os.remove(os.path.join(d, f))
     os.rmdir(d)
     return {"value": round(n / dt, 3), "unit": "ZMWs/s", "cores": threads, "affinity": affinity,
-            "nproc": os.cpu_count(), "kind": "port",
+            "cgroup_cpu_quota": quota, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "nproc": os.cpu_count(),
+            "kind": "port",
             "per_core_zmws_per_s": round(n1 / dt1, 3), "wall_s": round(dt, 3),
             "sample": f"config A end to end: {n} CCS from 1,000 ZMWs (10 kb x 8 passes, 10% error) read from FASTA, "
-                      f"ccs_prepare, POA and ordered output by oracle/ccsx_cpu -A -j {threads} (every CPU of the "
-                      f"process's affinity mask: {affinity}; nproc={os.cpu_count()}) in {dt:.2f} s; -j 1 on the first {sample_j1} ZMWs: {n1 / dt1:.2f} ZMWs/s. "
+                      f"ccs_prepare, POA and ordered output by oracle/ccsx_cpu -A -j {threads} (the CPUs the process "
+                      f"may use: affinity {affinity}, cgroup quota {quota or 'none'}, OMP_NUM_THREADS "
+                      f"{os.environ.get('OMP_NUM_THREADS')}; nproc={os.cpu_count()}) in {dt:.2f} s; -j 1 on the first {sample_j1} ZMWs: {n1 / dt1:.2f} ZMWs/s. "
                       "A scalar C restatement of SPEC.md + main.c, not bsalign's SIMD code (ccsx itself is "
                       "unbuildable here)"}
 

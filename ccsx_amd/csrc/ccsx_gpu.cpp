@@ -234,6 +234,11 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0)
             c->ncu = (uint32_t)n;
     }
+    // CCSX_KCFG forces a kernel configuration (A/B runs of the CLI / e2e)
+    if (const char *k = getenv("CCSX_KCFG")) {
+        const int v = atoi(k);
+        if (v >= -1 && v < ccsx::kCfgCount) c->cfg_force = v;
+    }
     if (e != hipSuccess) {
         fprintf(stderr, "[ccsx_gpu] cannot open device %d: %s\n", device, hipGetErrorString(e));
         for (Slot &s : c->slot) s.release();

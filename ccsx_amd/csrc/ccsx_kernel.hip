@@ -40,6 +40,20 @@
 namespace ccsx {
 namespace CCSX_KCFG {
 
+// CCSX_PEX_RING (the one-helper throughput configuration): wave 0 hands each
+// row's insertion prefix max (Pex, one word per lane) to the helper through
+// a small LDS ring instead of the helper re-running the 7-step DPP scan --
+// the helper, not wave 0, is that configuration's slower chain.  The ring
+// holds the helper's lag: two lockstep blocks.
+#ifndef CCSX_PEX_RING
+#define CCSX_PEX_RING 0
+#endif
+#ifndef CCSX_BLK
+#define CCSX_BLK 8
+#endif
+constexpr int kPexRing = CCSX_PEX_RING;
+constexpr int kPexRows = 2 * CCSX_BLK;
+
 constexpr int kO = -3, kE = -2, kMs = 2, kXs = -6;  // main.c:842-847
 enum { HC_MPRED = 0, HC_MSRC = 1, HC_DEL = 2, HC_INS = 3 };
 enum : uint32_t { EV_ALN = 0u, EV_INS = 1u, EV_LEAD = 2u };
@@ -274,7 +288,8 @@ constexpr int kLdsRing = 0;                              // kRingA DP rows x kRo
 constexpr int kLdsDiag = kLdsRing + kRingA * kRowW;      // 32: helpers' diagnostic counters at exit
 constexpr int kLdsOffRing = kLdsDiag + 32;               // 64: band offset of DP row q at q & 63
 constexpr int kLdsJob = kLdsOffRing + 64;                // 16: DP job / results
-constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
+constexpr int kLdsPex = kLdsJob + 16;                    // kPexRing: kPexRows rows x 64 lanes of Pex
+constexpr int kLdsFixed = kLdsPex + kPexRing * kPexRows * 64;  // then: the read (nibble pairs), shredding cursors
 
 
 // per lane: row r0+lane's info and first four predecessors
@@ -335,9 +350,6 @@ __device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; 
 
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
-#ifndef CCSX_BLK
-#define CCSX_BLK 8
-#endif
 constexpr int kBlkAB = CCSX_BLK;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2, ...
 // helper waves per workgroup: 2 (latency / occupancy configurations) or 1
 // (throughput configuration: two-wave workgroups, twice the resident ZMWs)
@@ -766,6 +778,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
+        if (kPexRing) z.lds[kLdsPex + (r % kPexRows) * 64 + lane] = Pex;  // for the helper (dpB_tail)
         // (inline asm measured 0.6 % faster than the compiler's writelane
         // intrinsic here: it keeps vOff / vKey out of the scheduler's way)
         S.vOff = writelane(S.vOff, off, li);
@@ -918,12 +931,6 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
     }
 }
 
-// helper rows per straight-line group (dpB_group); 0: one row at a time
-#ifndef CCSX_HGROUP
-#define CCSX_HGROUP 2
-#endif
-constexpr int kHGroup = CCSX_HGROUP;
-
 // helper wave: everything after the predecessor terms of row r (SPEC.md
 // §3.2-§3.5): M, H', the insertion scan, the cell codes and tags, the
 // free-end candidates, the record store
@@ -942,7 +949,8 @@ __device__ __forceinline__ void dpB_tail(Z &z, BState &S, uint32_t r, uint32_t m
     const int32_t hp0 = max(M0, A.Dv0), hp1 = max(M1, A.Dv1);
     // insertions (SPEC.md §3.4): the same prefix-max scan as wave 0's
     const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
-    const int32_t Pex = wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
+    const int32_t Pex = kPexRing ? z.lds[kLdsPex + (r % kPexRows) * 64 + lane]
+                                 : wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
     const int32_t X1L = wave_shr1(INT32_MAX, X1);
     const int32_t ex1 = max(Pex, X0);
     const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
@@ -969,16 +977,9 @@ __device__ __forceinline__ void dpB_tail(Z &z, BState &S, uint32_t r, uint32_t m
         if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
         if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
     }
-    // lexicographic (max e, min row, min cell): rows may come out of order
-    // (dpB_group: the other rows after the group's simple ones)
-    const uint32_t k0 = r * 2u, k1 = k0 + 1u;
-    if (kHGroup == 0) {  // rows in order: the first maximum is the earliest
-        if (e0 > S.bE) S.bE = e0, S.bKey = k0, S.bOff = off;
-        if (e1 > S.bE) S.bE = e1, S.bKey = k1, S.bOff = off;
-    } else {
-        if (e0 > S.bE || (e0 == S.bE && k0 < S.bKey)) S.bE = e0, S.bKey = k0, S.bOff = off;
-        if (e1 > S.bE || (e1 == S.bE && k1 < S.bKey)) S.bE = e1, S.bKey = k1, S.bOff = off;
-    }
+    // rows come in order: the first maximum is the earliest (min row, min cell)
+    if (e0 > S.bE) S.bE = e0, S.bKey = r * 2, S.bOff = off;
+    if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1, S.bOff = off;
     // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
     __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), S.rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
                                           0);
@@ -1031,119 +1032,6 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     DP_STAMP(kPfFlush);
 }
 
-// helper wave: G rows r0, r0 + st, ... as one straight-line group, so their
-// LDS round trips, DPP scans and stores overlap (a row alone is a chain of
-// two dependent LDS reads, a 7-step DPP chain and a store: ~1,600 cycles
-// issued one row after the other).  Covers the "simple" rows -- one or two
-// predecessors, both within the padded band, not far -- with the values of
-// dpB_row / pred_terms_n<NP, true> (the second predecessor of a one-
-// predecessor row re-reads the first, which never wins a strict > update;
-// D's slot and ext come from wave 0's D in the ring: slot 1 iff D > c0,
-// ext iff D > a of the chosen slot).  Any other row of the group is left to
-// dpB_row afterwards (the free-end candidates compare lexicographically, so
-// the order does not matter).
-template <bool FULL, int G>
-__device__ __forceinline__ void dpB_group(Z &z, BState &S, uint32_t r0, uint32_t st, uint32_t m, int32_t lim,
-                                          int32_t vOff, const LaneK &c)
-{
-    const int lane = lane_id();
-    const int32_t *ring = z.lds + kLdsRing;
-    constexpr int dd = kDc - kHc + 1;
-    uint32_t simple = 0;  // bit g: row g takes this path
-    int32_t off[G];
-    uint32_t r[G], base[G], tag0[G], tag1[G], two[G];
-    const int32_t *pa[G], *pb[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        r[g] = r0 + (uint32_t)g * st;
-        const int li = (int)(r[g] & 63u);
-        const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
-        const uint32_t np = info >> 8;
-        off[g] = __builtin_amdgcn_readlane(vOff, li);
-        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
-        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
-        const int32_t sh0 = off[g] - __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
-        const int32_t sh1 = off[g] - __builtin_amdgcn_readlane(vOff, (int)(p1 & 63u));
-        const bool ok = r[g] < z.R && !(info & kInfoFar) && (np == 1u || np == 2u) && (uint32_t)(sh0 + 3) <= 7u &&
-                        (np == 1u || (uint32_t)(sh1 + 3) <= 7u);
-        simple |= ok ? 1u << g : 0u;
-        two[g] = np == 2u ? 1u : 0u;
-        const uint32_t q1 = np == 2u ? p1 : p0;
-        base[g] = info & 3u;
-        tag0[g] = r[g] - p0;
-        tag1[g] = r[g] - q1;
-        // (a row off this path reads row p0 at shift 0: in range, unused)
-        pa[g] = ring + (p0 % kRingA) * kRowW + (kHc - 1) + c.L2 + (ok ? sh0 : 0);
-        pb[g] = ring + (q1 % kRingA) * kRowW + (kHc - 1) + c.L2 + (ok ? (np == 2u ? sh1 : sh0) : 0);
-    }
-    simple = uni(simple);
-    // every LDS read of the group first
-    uint32_t qp[G];
-    int32_t Dv0[G], Dv1[G], hA0[G], hB0[G], hC0[G], dB0[G], dC0[G], hA1[G], hB1[G], hC1[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        qp[g] = (uint32_t)z.rd[(off[g] >> 1) + lane] >> ((uint32_t)(off[g] & 1) * 4u);
-        const int2 Dv = reinterpret_cast<const int2 *>(ring + (r[g] % kRingA) * kRowW + kDc + c.L2)[0];
-        Dv0[g] = Dv.x, Dv1[g] = Dv.y;
-        hA0[g] = pa[g][0], hB0[g] = pa[g][1], hC0[g] = pa[g][2], dB0[g] = pa[g][dd], dC0[g] = pa[g][dd + 1];
-        hA1[g] = pb[g][0], hB1[g] = pb[g][1], hC1[g] = pb[g][2];
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        // M (first maximal predecessor on ties), D's slot and ext
-        const bool m0 = hA1[g] > hA0[g], m1 = hB1[g] > hB0[g];
-        const int32_t Mh0 = m0 ? hA1[g] : hA0[g], Mh1 = m1 ? hB1[g] : hB0[g];
-        const uint32_t ms0 = m0 ? tag1[g] : tag0[g], ms1 = m1 ? tag1[g] : tag0[g];
-        const int32_t c0 = max(hB0[g] + (kO + kE), dB0[g] + kE), c1 = max(hC0[g] + (kO + kE), dC0[g] + kE);
-        const bool s0 = two[g] && Dv0[g] > c0, s1 = two[g] && Dv1[g] > c1;
-        const uint32_t ds0 = s0 ? tag1[g] : tag0[g], ds1 = s1 ? tag1[g] : tag0[g];
-        const uint32_t dx0 = Dv0[g] > (s0 ? hB1[g] : hB0[g]) + (kO + kE) ? 4u : 0u;
-        const uint32_t dx1 = Dv1[g] > (s1 ? hC1[g] : hC0[g]) + (kO + kE) ? 4u : 0u;
-        // dpB_tail's values (no wide records: np <= 2)
-        const int32_t o = off[g];
-        const int32_t srcu = c.src0 + kE * o;
-        const int32_t src0 = (o == 0 && lane == 0) ? 0 : srcu;
-        const bool mp0 = Mh0 >= src0, mp1 = Mh1 >= srcu + kE;
-        const int32_t M0 = max(Mh0, src0) + ((qp[g] & 3u) == base[g] ? kMs : kXs);
-        const int32_t M1 = max(Mh1, srcu + kE) + (((qp[g] >> 2) & 3u) == base[g] ? kMs : kXs);
-        const bool d0 = Dv0[g] > M0, d1 = Dv1[g] > M1;
-        const int32_t hp0 = max(M0, Dv0[g]), hp1 = max(M1, Dv1[g]);
-        const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
-        const int32_t Pex = wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
-        const int32_t X1L = wave_shr1(INT32_MAX, X1);
-        const int32_t ex1 = max(Pex, X0);
-        const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
-        const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
-        const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
-        const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
-        uint32_t w0 = hc0 | dx0 | iext0 | ((ms0 & 63u) << 4) | ((ds0 & 63u) << 10);
-        uint32_t w1 = hc1 | dx1 | iext1 | ((ms1 & 63u) << 4) | ((ds1 & 63u) << 10);
-        const int32_t eb = 2 * o - 2 * (int32_t)m - 1;
-        int32_t e0 = X0 + eb;
-        int32_t e1 = X1 + eb;
-        if (FULL) {
-            e1 += (o == lim && lane == 63) ? 3 : 0;
-        } else {
-            if ((uint32_t)c.L2 == m - 1) e0 += 3;
-            if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
-            if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
-            if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
-        }
-        const bool ok = (simple >> g) & 1u;
-        if (!ok) e0 = e1 = INT32_MIN;
-        const uint32_t k0 = r[g] * 2u, k1 = k0 + 1u;
-        if (e0 > S.bE || (e0 == S.bE && k0 < S.bKey)) S.bE = e0, S.bKey = k0, S.bOff = o;
-        if (e1 > S.bE || (e1 == S.bE && k1 < S.bKey)) S.bE = e1, S.bKey = k1, S.bOff = o;
-        // (a row off this path stores out of the buffer's range: dropped)
-        __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), S.rc,
-                                              ok ? r[g] * 256u + (((uint32_t)lane * 4u + tb_rot(r[g])) & 255u) : ~0u, 0, 0);
-    }
-    // the rest of the group's rows, one at a time
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-        if (!((simple >> g) & 1u) && r[g] < z.R) dpB_row<FULL>(z, S, r[g], m, lim, vOff, c);
-}
-
 // helper wave h: rows r0 + h + 2i of the block [r0, r0 + kBlkAB); wave 1 also
 // writes the row meta words {band offset | far << 31} of each 16-row group
 template <bool FULL>
@@ -1154,20 +1042,9 @@ __device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t
     const int32_t lim = FULL ? (int32_t)m - kW : 0;
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
-    // this helper's rows r0 + h + kHelpers i, in groups of kHGroup (0: one
-    // row at a time)
-    constexpr int kRowsPerHelper = kBlkAB / kHelpers;
-    if (kHGroup == 0) {
 #pragma unroll
-        for (uint32_t i = h; i < (uint32_t)kBlkAB; i += kHelpers)
-            if (r0 + i < R) dpB_row<FULL>(z, S, r0 + i, m, lim, vOff, c);
-    } else {
-        constexpr int G = kHGroup ? kHGroup : 1;
-        static_assert(kRowsPerHelper % G == 0, "a helper's rows of a block form whole groups");
-#pragma unroll
-        for (int g = 0; g < kRowsPerHelper; g += G)
-            dpB_group<FULL, G>(z, S, r0 + h + (uint32_t)(g * kHelpers), kHelpers, m, lim, vOff, c);
-    }
+    for (uint32_t i = h; i < (uint32_t)kBlkAB; i += kHelpers)
+        if (r0 + i < R) dpB_row<FULL>(z, S, r0 + i, m, lim, vOff, c);
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
     if (h == 0 && ((r0 & 15u) == 16u - kBlkAB || rend == R)) {
         const uint32_t g0 = r0 & ~15u;
