@@ -36,7 +36,9 @@ KCFGS = [(n, [f"-DCCSX_KCFG={n}", f"-DCCSX_LAUNCH=ccsx_launch_zmw_{n}", f"-DCCSX
          for n, d in [("lat", ["-DCCSX_RINGA=32", "-DCCSX_BLK=8"]),
                       ("occ", ["-DCCSX_RINGA=24", "-DCCSX_BLK=4"]),
                       # two-wave workgroups, a 16-row ring read back 8 rows
-                      ("tput", ["-DCCSX_RINGA=16", "-DCCSX_BLK=4", "-DCCSX_RING=8", "-DCCSX_HELPERS=1"])]]
+                      # no issue priorities: two wave 0s share each SIMD (A/B r03g: D 567 -> 550 ms)
+                      ("tput", ["-DCCSX_RINGA=16", "-DCCSX_BLK=4", "-DCCSX_RING=8", "-DCCSX_HELPERS=1",
+                                "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0"])]]
 
 
 def _hipcc() -> str:

@@ -293,6 +293,9 @@ constexpr size_t kPinnedSeqFloor = 512ull << 20, kPinnedOutFloor = 128ull << 20;
 constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
 // LDS read buffer of a tight-cap shredded slice (bases)
 constexpr uint32_t kShredReadCap = 8192;
+// slices of at least this many times the occupancy configuration's resident
+// workgroups run the throughput configuration
+constexpr size_t kTputSliceFactor = 3;
 
 // launch classes of ccsx_gpu_run's slices: LDS read buffer up to 32 kb (4+
 // workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never
@@ -395,12 +398,19 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
         s.lds_read_words = (lb + 7) / 8 + 2;
         s.lds_nmax = std::max<uint32_t>(nmax, 1);
     }
-    // kernel configuration: the latency one if it keeps the whole slice
-    // resident, else the occupancy one (ccsx_layout.h KernelCfg)
+    // kernel configuration (ccsx_layout.h KernelCfg): the latency one if it
+    // keeps the whole slice resident; the throughput one (two-wave
+    // workgroups) once the slice is several times what the occupancy one
+    // keeps resident, so the launch is bound by resident ZMWs rather than by
+    // its slowest ZMW's chain (which is ~27 % longer there); the occupancy
+    // one in between
     {
         const uint32_t extra = s.lds_read_words + s.lds_nmax;
         const size_t res_lat = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgLatency, extra);
-        s.cfg = c->cfg_force >= 0 ? c->cfg_force : (nz <= res_lat ? ccsx::kCfgLatency : ccsx::kCfgOccupancy);
+        const size_t res_occ = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgOccupancy, extra);
+        s.cfg = nz <= res_lat ? ccsx::kCfgLatency : nz < kTputSliceFactor * res_occ ? ccsx::kCfgOccupancy
+                                                                                  : ccsx::kCfgThroughput;
+        if (c->cfg_force >= 0) s.cfg = c->cfg_force;
     }
     size_t freeb = 0, totb = 0;
     const auto ti = std::chrono::steady_clock::now();

@@ -10,6 +10,7 @@
 #   bench              the default bench.py line (config B, 20 steps, e2e, cpu baseline)
 #   bench:CFG[:KCFG]   bench.py --config CFG (B|C|D|E|H), 3 steps, optional forced kernel cfg
 #   ab:CFG:KCFG,...[:LIB,...]  3 interleaved rounds of bench --config CFG over kernel cfgs x libraries
+#   e2e:N[:KCFG]       bench.py's end-to-end line (config E, ccsx_gpu_run) on N ZMWs per GPU
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
@@ -61,6 +62,11 @@ step() {
           done
         done
       done ;;
+    e2e)  # e2e:N[:KCFG] -- bench.py's config-E end-to-end line on N ZMWs (CCSX_KCFG forces a kernel cfg)
+      local f="$OUT/e2e_${cfg}${k:+_k$k}.json"
+      CCSX_KCFG=${k:--1} CCSX_TIMING=1 timeout -k 10 600 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline \
+        --e2e-zmws "$cfg" > "$f" 2> "${f%.json}.err" &&
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1]))['e2e']; print(sys.argv[1], d['value'], 'ZMWs/s', d['s'], 's', d['gcups'], 'GCUPS', 'first', d['first_call_s'])" "$f" ;;
     kt)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_$cfg" -o kt -- \
         python3 "$R/bench.py" --config "$cfg" --no-cpu-baseline --e2e-zmws 0 > "$OUT/kt_$cfg.json" 2> "$OUT/kt_$cfg.err") &&
