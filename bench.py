@@ -33,6 +33,12 @@ CONFIGS = {
               nzmw=1000, L=20000, passes=5, mode=1),
     "D": dict(workload="D: 10000 ZMWs x 2 kb insert x 30 passes, 10% error, shredded mode",
               nzmw=10000, L=2000, passes=30, mode=0),
+    # subreads beyond the LDS read buffer (100 kb): the HBM-read kernel
+    # instance (not a BASELINE config; 440 kb per ZMW stays under -M 500000)
+    "H": dict(workload="H: 256 ZMWs x 110 kb insert x 4 passes, 10% error, shredded mode (HBM-read kernel instance)",
+              nzmw=256, L=110000, passes=4, mode=0),
+    "HP": dict(workload="HP: 256 ZMWs x 110 kb insert x 4 passes, 10% error, primitive (-P) mode "
+                        "(HBM-read kernel instance)", nzmw=256, L=110000, passes=4, mode=1),
     # a per-GPU slice of config E (500k ZMWs, mixed 5-25 kb inserts, 5-12 passes)
     "E": dict(workload="E-slice: 2000 ZMWs per GPU, insert ~U[5,25] kb x passes ~U[5,12] (total <= 450 kb), "
                        "10% error, shredded mode", nzmw=2000, L=0, passes=0, mode=0),

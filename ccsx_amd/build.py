@@ -148,6 +148,12 @@ def build_product(verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
+    # tools/synth_fa: the synthetic subread FASTA streamer (CLI runs at config-E scale)
+    gsrc = os.path.join(ROOT, "tools", "synth_fa.c")
+    gexe = os.path.join(ROOT, "tools", "synth_fa")
+    if os.path.exists(gsrc) and _stale(gexe, [gsrc, LIB]):
+        _run(["gcc", "-O2", "-std=gnu11", "-I" + INC, "-o", gexe, gsrc, "-L" + HERE, "-lccsx_amd",
+              "-Wl,-rpath,$ORIGIN/../ccsx_amd", "-lpthread"])
     return LIB
 
 

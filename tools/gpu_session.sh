@@ -14,7 +14,7 @@
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
-#   cli:N              CLI end to end on N config-E ZMWs streamed on stdin (tools/cli_e2e.py)
+#   cli:N[:pipe]       CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py)
 #   lib:NAME           the following steps load ccsx_amd/NAME (CCSX_LIB); lib: resets
 # Environment: CCSX_LIB selects a library variant for the bench steps.
 set -o pipefail
@@ -78,9 +78,10 @@ step() {
       timeout -k 10 600 python -u tools/phase_prof.py --L "$L" --passes "$P" --n "$N" --kcfg "${k:--1}" \
         > "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" 2> "$OUT/phase.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['kernel_ms'],2), 'ms', d['share'], d.get('two_wave'))" "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" ;;
-    cli)
-      timeout -k 10 900 python -u tools/cli_e2e.py --n "$cfg" --out "$OUT" > "$OUT/cli_$cfg.log" 2>&1; local rc=$?
-      tail -5 "$OUT/cli_$cfg.log"; return $rc ;;
+    cli)  # cli:N[:pipe] -- tools/cli_stream.py: the CLI on N config-E ZMWs on stdin + oracle sample check
+      timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" ${k:+--pipe} --out "$OUT/cli_$cfg${k:+_$k}" \
+        > "$OUT/cli_$cfg${k:+_$k}.log" 2>&1; local rc=$?
+      tail -5 "$OUT/cli_$cfg${k:+_$k}.log"; return $rc ;;
     lib)  # lib:NAME -- later steps load ccsx_amd/NAME (lib: = the product library)
       if [ -n "$cfg" ]; then export CCSX_LIB=$cfg; else unset CCSX_LIB; fi ;;
     *) echo "unknown step $s"; return 2 ;;
