@@ -86,6 +86,8 @@ int usage()
             "               GPUs places group g on GPU g %% visible (logical contexts)\n"
             "CCSX_SLOTS     Device contexts (worker threads) per group [1]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
+            "CCSX_CHUNK     Largest chunk in ZMWs [16384 x min(groups, 4)]\n"
+            "CCSX_KCFG      Force a kernel configuration (0 latency, 1 occupancy, 2 throughput)\n"
             "\n"
             "Arguments:\n"
             "input          Input file.\n"
@@ -451,7 +453,8 @@ int main(int argc, char **argv)
     // step 0 (main.c:652-697) + the CPU half of step 1; the reference grows
     // the chunk 1,024 -> 4,096 -> 16,384 ZMWs (main.c:686-690), here the
     // last size scales with the devices (output order does not depend on it)
-    const size_t chunk_max = 16384u * (size_t)std::min(ngroup, 4);
+    size_t chunk_max = 16384u * (size_t)std::min(ngroup, 4);
+    if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));
     size_t chunk_size = 1024;
     for (size_t id = 0; !fatal; ++id) {
         auto ch = std::make_shared<Chunk>();

@@ -15,6 +15,7 @@
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
 #   cli:N[:pipe]       CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py)
+#   env:NAME=VALUE     export NAME for the following steps (env:NAME= unsets it)
 #   lib:NAME           the following steps load ccsx_amd/NAME (CCSX_LIB); lib: resets
 # Environment: CCSX_LIB selects a library variant for the bench steps.
 set -o pipefail
@@ -79,9 +80,11 @@ step() {
         > "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" 2> "$OUT/phase.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['kernel_ms'],2), 'ms', d['share'], d.get('two_wave'))" "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" ;;
     cli)  # cli:N[:pipe] -- tools/cli_stream.py: the CLI on N config-E ZMWs on stdin + oracle sample check
-      timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" ${k:+--pipe} --out "$OUT/cli_$cfg${k:+_$k}" \
-        > "$OUT/cli_$cfg${k:+_$k}.log" 2>&1; local rc=$?
-      tail -5 "$OUT/cli_$cfg${k:+_$k}.log"; return $rc ;;
+      local tag="cli_$cfg${k:+_$k}${CCSX_SLOTS:+_s$CCSX_SLOTS}${CCSX_CHUNK:+_c$CCSX_CHUNK}"
+      timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" ${k:+--pipe} --out "$OUT/$tag" > "$OUT/$tag.log" 2>&1
+      local rc=$?; tail -5 "$OUT/$tag.log"; return $rc ;;
+    env)  # env:NAME=VALUE -- export for the following steps (env:NAME= unsets)
+      if [ -n "${cfg#*=}" ]; then export "$cfg"; else unset "${cfg%%=*}"; fi ;;
     lib)  # lib:NAME -- later steps load ccsx_amd/NAME (lib: = the product library)
       if [ -n "$cfg" ]; then export CCSX_LIB=$cfg; else unset CCSX_LIB; fi ;;
     *) echo "unknown step $s"; return 2 ;;
