@@ -459,6 +459,9 @@ int main(int argc, char **argv)
     // step 0 (main.c:652-697) + the CPU half of step 1; the reference grows
     // the chunk 1,024 -> 4,096 -> 16,384 ZMWs (main.c:686-690), here the
     // last size scales with the devices (output order does not depend on it)
+    // micro-batches per context and chunk (CCSX_CTX_BATCHES, default 2)
+    uint32_t batches_per_ctx = 2;
+    if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
     size_t chunk_max = 16384u * (size_t)std::min(ngroup, 4);
     if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));
     size_t chunk_size = 1024;
@@ -492,7 +495,8 @@ int main(int argc, char **argv)
         std::vector<uint64_t> cost(n);
         for (uint32_t i = 0; i < n; ++i) cost[i] = ccsx_zmw_cost(zs[i].seg_len.data(), (uint32_t)zs[i].seg_len.size());
         std::vector<uint32_t> order(n), bounds(n + 1);
-        const uint32_t nb = ccsx_partition(cost.data(), n, (uint32_t)nctx * 2u, 256u, order.data(), bounds.data());
+        const uint32_t nb = ccsx_partition(cost.data(), n, (uint32_t)nctx * batches_per_ctx, 256u, order.data(),
+                                           bounds.data());
         std::vector<Batch> bs(nb);
         for (uint32_t b = 0; b < nb; ++b) {
             bs[b].chunk = ch;
