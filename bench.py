@@ -259,7 +259,7 @@ def main():
         eng.set_mem_share(sharing)
     if args.kcfg >= 0:
         eng.set_kernel_cfg(args.kcfg)
-    eng.stage(zs)
+    eng.stage(zs, cfg["mode"])  # the capacities ccsx_gpu_run uses for the mode
     for _ in range(args.warmup):
         eng.launch(cfg["mode"])
 

@@ -146,7 +146,7 @@ struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     size_t nz = 0;
-    uint32_t lds_read_words = 0, lds_nmax = 0;
+    uint32_t lds_read_words = 0, lds_nmax = 0, lds_extra = 0;
     int32_t cfg = ccsx::kCfgLatency;   // kernel configuration of the staged slice
     uint64_t seq_bytes = 0, ws_bytes = 0, out_bytes = 0, msa_bytes = 0, bp_words = 0;
     uint32_t nseg_total = 0;
@@ -300,11 +300,16 @@ constexpr size_t kTputSliceFactor = 3;
 // launch classes of ccsx_gpu_run's slices: LDS read buffer up to 32 kb (4+
 // workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never
 // mix classes, so one long read does not shrink the occupancy of a slice
-static int zmw_class(const ccsx_zmw_in &zi)
+// (shred_tight: a tight-cap shredded slice, whose LDS read buffer holds
+// kShredReadCap bases whatever the segment lengths -- pushed windows are
+// 2-10 kb -- so only the cursor count sends it to the HBM-read instance)
+static int zmw_class(const ccsx_zmw_in &zi, bool shred_tight)
 {
     uint32_t lmax = 0;
     for (uint32_t k = 0; k < zi.nseg; ++k) lmax = std::max(lmax, zi.seg_len[k]);
-    if (lmax > kLdsReadMaxBases || zi.nseg > kLdsMaxSegs) return 2;
+    if (zi.nseg > kLdsMaxSegs) return 2;
+    if (shred_tight) return 0;
+    if (lmax > kLdsReadMaxBases) return 2;
     return lmax > 32768 ? 1 : 0;
 }
 
@@ -384,7 +389,8 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
     // every lane reads its window bytes even when the read is shorter.  A
     // slice with a read or a cursor array beyond the LDS budget runs the
     // HBM-read kernel instance (lds_read_words = 0)
-    if (lmax_all > kLdsReadMaxBases || nmax > kLdsMaxSegs) {
+    const bool shred_tight = c->shred_caps && !full_caps;
+    if (nmax > kLdsMaxSegs || (lmax_all > kLdsReadMaxBases && !shred_tight)) {
         s.lds_read_words = 0;
         s.lds_nmax = 0;
     } else {
@@ -394,10 +400,13 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
         // uncapped), which keeps the LDS of config-E slices small enough for
         // one more workgroup per CU
         uint32_t lb = std::max<uint32_t>(lmax_all, ccsx::kW);
-        if (c->shred_caps && !full_caps) lb = std::min(lb, kShredReadCap);
+        if (shred_tight) lb = std::min(lb, kShredReadCap);
         s.lds_read_words = (lb + 7) / 8 + 2;
         s.lds_nmax = std::max<uint32_t>(nmax, 1);
     }
+    // LDS words after the configuration's fixed part: the read buffer and
+    // the cursors, or the HBM-read instance's read window
+    s.lds_extra = s.lds_read_words ? s.lds_read_words + s.lds_nmax : ccsx::kRdWinBytes / 4;
     // kernel configuration (ccsx_layout.h KernelCfg): the latency one if it
     // keeps the whole slice resident; the throughput one (two-wave
     // workgroups) once the slice is several times what the occupancy one
@@ -405,7 +414,7 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
     // its slowest ZMW's chain (which is ~27 % longer there); the occupancy
     // one in between
     {
-        const uint32_t extra = s.lds_read_words + s.lds_nmax;
+        const uint32_t extra = s.lds_extra;
         const size_t res_lat = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgLatency, extra);
         const size_t res_occ = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgOccupancy, extra);
         s.cfg = nz <= res_lat ? ccsx::kCfgLatency : nz < kTputSliceFactor * res_occ ? ccsx::kCfgOccupancy
@@ -502,7 +511,7 @@ static int launch_slot(ccsx_ctx *c, Slot &s, int mode)
         HIPCHK(c, s.d_prof.reserve(s.nz * ccsx::kProfSlots * 8));
         a.prof = s.d_prof.as<unsigned long long>();
     }
-    const uint32_t lds = kcfg_lds(s.cfg, s.lds_read_words + s.lds_nmax);
+    const uint32_t lds = kcfg_lds(s.cfg, s.lds_extra);
     if (lds > 160 * 1024) {
         c->err = "reads too long for the LDS read buffer";
         return -1;
@@ -571,6 +580,19 @@ int ccsx_gpu_stage_ex(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz, int with_msa
 }
 
 int ccsx_gpu_stage(ccsx_ctx *c, const ccsx_zmw_in *z, size_t nz) { return ccsx_gpu_stage_ex(c, z, nz, 0, 0); }
+
+int ccsx_gpu_stage_for(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz)
+{
+    if (!c) return -1;
+    if (mode != CCSX_MODE_SHRED && mode != CCSX_MODE_PRIMITIVE) {
+        c->err = "mode must be CCSX_MODE_SHRED or CCSX_MODE_PRIMITIVE";
+        return -1;
+    }
+    c->shred_caps = mode == CCSX_MODE_SHRED;
+    const int r = ccsx_gpu_stage_ex(c, z, nz, 0, 0);
+    c->shred_caps = false;
+    return r;
+}
 
 int ccsx_gpu_launch_ex(ccsx_ctx *c, int mode, float *kernel_ms)
 {
@@ -765,11 +787,12 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     std::vector<uint32_t> all(nz), retry;
     std::vector<uint64_t> cost(nz);
     for (size_t i = 0; i < nz; ++i)
-        all[i] = uint32_t(i), cls[i] = zmw_class(z[i]), cost[i] = ccsx_zmw_cost(z[i].seg_len, z[i].nseg);
+        all[i] = uint32_t(i), cls[i] = zmw_class(z[i], c->shred_caps), cost[i] = ccsx_zmw_cost(z[i].seg_len, z[i].nseg);
     std::stable_sort(all.begin(), all.end(),
                      [&](uint32_t x, uint32_t y) { return cls[x] != cls[y] ? cls[x] < cls[y] : cost[x] > cost[y]; });
     int r = run_list(all, false, &retry);
     if (!r && !retry.empty()) {
+        for (uint32_t g : retry) cls[g] = zmw_class(z[g], false);  // full caps: whole segments in the buffer
         if (timing) fprintf(stderr, "[ccsx_gpu_run] dev %d: %zu ZMWs re-run with full caps\n", c->device, retry.size());
         c->reruns += retry.size();
         r = run_list(retry, true, nullptr);

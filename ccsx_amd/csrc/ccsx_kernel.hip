@@ -174,6 +174,12 @@ struct Z {
     const uint8_t *seq;
     int32_t *lds;        // workgroup LDS: DP ring (kRingA rows x kRowW words), offsets, job, read
     uint8_t *rd;         // read as nibble pairs: byte b = pair(2b) | pair(2b+1) << 4, pair(j) = code(j) | code(j+1) << 2
+    // HBM-read instance: an LDS window of the read (rd_window), two chunks of
+    // kWinChunk bases resident, the first one wa (wave 0's view)
+    uint8_t *win;
+    bool hbm;
+    uint32_t wa, rdbytes;
+    bool wpend;  // wave 0: chunk wa + 1 is to be loaded at the next block's start
     uint32_t *pos;       // shredding cursors
     uint32_t rdcap;      // bases that fit in rd
     int cur;
@@ -252,6 +258,49 @@ __device__ __forceinline__ uint32_t *G_poff(const Z &z, int b) { return P<uint32
 __device__ __forceinline__ uint32_t *G_pred(const Z &z, int b) { return P<uint32_t>(z, b ? z.L.pred1 : z.L.pred0); }
 
 __device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return ((uint32_t)z.rd[j >> 1] >> ((j & 1u) * 4u)) & 3u; }
+
+// ----------------------------------------------------------------------------
+// The HBM-read instance's read window.  Reads beyond the LDS read buffer live
+// in the workspace; a DP row reads the bytes of its band [off, off + 130)
+// once per row (wave 0 a row ahead, each helper for its own rows), which from
+// HBM is a global round trip on every row.  So two consecutive chunks of
+// kWinChunk bases (chunk c in ring half c & 1) are kept in LDS; when wave 0's
+// band enters the upper chunk at the end of a block it publishes the slide
+// (job word wa << 1 | 1) and loads the next chunk at the start of its next
+// block, over the half that held the chunk below.  During that period the
+// helpers (one block behind) trust only the kept chunk; a row outside what
+// its wave may trust reads HBM (rare: a band far behind the diagonal).
+// ----------------------------------------------------------------------------
+constexpr uint32_t kWinBytesMask = kRdWinBytes - 1;
+
+__device__ __forceinline__ void win_load(const Z &z, uint32_t c)
+{
+    const uint32_t lane = lane_id();
+    const auto rs = brsrc(z.rd, z.rdbytes);  // beyond the buffer: zeros
+#pragma unroll
+    for (uint32_t k = 0; k < kWinChunk / 2 / 1024; ++k) {
+        const uint32_t b = c * (kWinChunk / 2) + k * 1024 + lane * 16;
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, b, 0, 0);
+        *reinterpret_cast<v4u *>(z.win + (b & kWinBytesMask)) = v;
+    }
+    wsync();
+}
+
+// bases [off, off + 132) within chunks [c0, c0 + nc) (uniform)
+__device__ __forceinline__ bool win_has(uint32_t c0, uint32_t nc, int32_t off)
+{
+    return (uint32_t)off >= c0 * kWinChunk && (uint32_t)off + 132u <= (c0 + nc) * kWinChunk;
+}
+
+// lane's byte (off >> 1) + lane + d of the read (the LDS buffer, or the
+// window / HBM on the HBM-read instance; `inwin`: the wave may trust the
+// window for this row)
+__device__ __forceinline__ uint32_t rd_byte(const Z &z, int32_t off, uint32_t d, bool inwin)
+{
+    const uint32_t b = (uint32_t)(off >> 1) + lane_id() + d;
+    if (!z.hbm) return z.rd[b];
+    return inwin ? z.win[b & kWinBytesMask] : z.rd[b];
+}
 
 // ----------------------------------------------------------------------------
 // push: stage read k (ASCII in HBM) into LDS as nibble pairs: the byte at
@@ -378,6 +427,7 @@ struct DpJob {
     uint32_t m, R, cur;
     uint32_t k;     // merge: read index
     uint32_t K, E;  // merge: new rows (wave 0's M1), edges of the new graph
+    uint32_t win;   // DP on the HBM-read instance: first resident window chunk << 1 | slide in progress
     // results of helper wave 1 + h (h = row parity): best free-end value, its
     // row and read position, status
     struct {
@@ -731,7 +781,6 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t base = info & 3u;
     const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
-    const uint8_t *rdl = z.rd + lane;
     const int32_t pb = S.pOff & ~1;  // S.qn: read bytes (pOff >> 1) + lane, + 1
     const int32_t sh = coff - S.pOff;
     // (an integer test keeps the branch scalar: a bool of && lowers to a lane mask)
@@ -747,7 +796,10 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
                     bool cold) __attribute__((always_inline)) {
         // the next row's read window, a row ahead of its use (its offset lies
         // in [off, off + 3] on every fast row)
-        S.qn = (uint32_t)rdl[off >> 1] | (uint32_t)rdl[(off >> 1) + 1] << 8;
+        {
+            const bool w = z.hbm && win_has(z.wa, 2, off);
+            S.qn = rd_byte(z, off, 0, w) | rd_byte(z, off, 1, w) << 8;
+        }
         const uint32_t q0 = qp & 3u, q1 = (qp >> 2) & 3u;
         const int32_t srcu = c.src0 + kE * off;
         // (the fast rows fold the j = 0 leading term into Mh0, see below)
@@ -857,7 +909,8 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
 #endif
         (void)kind;
         const uint32_t d = (uint32_t)(off - pb);
-        const uint32_t qp = d <= 3u ? S.qn >> (4u * d) : (uint32_t)rdl[off >> 1] >> ((uint32_t)(off & 1) * 4u);
+        const uint32_t qp =
+            d <= 3u ? S.qn >> (4u * d) : rd_byte(z, off, 0, z.hbm && win_has(z.wa, 2, off)) >> ((uint32_t)(off & 1) * 4u);
         tail(off, qp, Mh0, Mh1, Dv0, Dv1, true);
     }
 }
@@ -893,6 +946,7 @@ struct BState {
     int32_t bE;       // best free-end value of this lane's cells
     uint32_t bKey;    // its row * 2 + cell
     int32_t bOff;     // its row's band offset
+    uint32_t wc0, wnc;  // HBM-read instance: the read-window chunks this period may trust
     RecWin W;
     __amdgpu_buffer_rsrc_t rc;  // cell records of this DP (R rows x 256 B)
 };
@@ -1002,7 +1056,7 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t np = info >> 8;
     const int32_t off = __builtin_amdgcn_readlane(vOff, li);
-    const uint32_t qp = (uint32_t)z.rd[(off >> 1) + lane] >> ((uint32_t)(off & 1) * 4u);
+    const uint32_t qp = rd_byte(z, off, 0, z.hbm && win_has(S.wc0, S.wnc, off)) >> ((uint32_t)(off & 1) * 4u);
     const int2 Dv = reinterpret_cast<const int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kDc + c.L2)[0];
     PredAcc A;
     A.Dv0 = Dv.x, A.Dv1 = Dv.y;
@@ -1068,12 +1122,17 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
         z.lds[kLdsRing + (i >> 4) * kRowW + w] = k < 8 ? kNegH : kNeg;
     }
     volatile DpJob *job = dp_job(z);
-    if (lane == 0) job->kind = kJobDp, job->m = m, job->R = z.R, job->cur = (uint32_t)z.cur;
+    if (z.hbm) {  // the read's first two window chunks
+        z.wa = 0, z.wpend = false;
+        win_load(z, 0);
+        win_load(z, 1);
+    }
+    if (lane == 0) job->kind = kJobDp, job->m = m, job->R = z.R, job->cur = (uint32_t)z.cur, job->win = 0;
     __syncthreads();  // J: job posted
     AState S;
     S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
     S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
-    S.qn = (uint32_t)z.rd[lane] | (uint32_t)z.rd[lane + 1] << 8;
+    S.qn = rd_byte(z, 0, 0, true) | rd_byte(z, 0, 1, true) << 8;
     S.nspill = 0;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
@@ -1082,7 +1141,19 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
     unsigned long long t_prev = stamp();
 #endif
     for (uint32_t b = 0; b <= nblk; ++b) {
-        if (b < nblk) dpA_block<FULL>(z, S, b * kBlkAB, m);
+        if (b < nblk) {
+            if (z.hbm && z.wpend) {  // the slide published at the last barrier
+                win_load(z, z.wa + 1);
+                z.wpend = false;
+            }
+            dpA_block<FULL>(z, S, b * kBlkAB, m);
+            if (z.hbm) {
+                // the block's last band entered the upper chunk: slide
+                z.wpend = (uint32_t)S.pOff >= (z.wa + 1) * kWinChunk;
+                z.wa += z.wpend ? 1u : 0u;
+                if (lane == 0) job->win = z.wa << 1 | (z.wpend ? 1u : 0u);
+            }
+        }
         DP_STAMP(kPfAbusy);
         lds_barrier();
         DP_STAMP(kPfAwait);
@@ -1113,6 +1184,7 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
     const int lane = lane_id();
     BState S;
     S.bE = INT32_MIN, S.bKey = 0, S.bOff = 0;
+    S.wc0 = 0, S.wnc = 2;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
     S.rc = brsrc(z.ws + z.L.codes, z.R * 256u);
@@ -1122,6 +1194,10 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
 #endif
     // period b: the decision bits of block b-1
     for (uint32_t b = 0; b <= nblk; ++b) {
+        if (z.hbm) {  // the window state wave 0 published at the last barrier
+            const uint32_t w = uni(dp_job(z)->win);
+            S.wc0 = w >> 1, S.wnc = (w & 1u) ? 1u : 2u;
+        }
         if (b >= 1 && !z.status) dpB_block<FULL>(z, S, (b - 1) * kBlkAB, m, h, z.lds[kLdsOffRing + lane]);
         if (b == nblk) {
             // this wave's candidate: lexicographic (max score, min row, min j)
@@ -2303,6 +2379,10 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
     z.ws = a.ws + z.d.ws_off;
     z.seq = a.seq + z.d.seq_off;
     z.lds = smem;
+    z.hbm = RD_HBM;
+    z.wa = 0, z.wpend = false;
+    z.win = reinterpret_cast<uint8_t *>(smem + kLdsFixed);
+    z.rdbytes = (uint32_t)zext_size(z.d, kExtRdbuf);
     if (RD_HBM) {
         z.rd = PX<uint8_t>(z, kExtRdbuf);
         z.pos = PX<uint32_t>(z, kExtPos);

@@ -33,6 +33,10 @@ constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H a
 // 57.0 for 24 rows and 4-row blocks, tools/gpu_ab.sh r02o)
 constexpr int kRingA = CCSX_RINGA;
 constexpr int kNeg = -(1 << 29);
+// the HBM-read kernel instance's LDS window of the read: two chunks of
+// kWinChunk bases as nibble pairs (ccsx_kernel.hip win_load)
+constexpr uint32_t kWinChunk = 8192;
+constexpr uint32_t kRdWinBytes = kWinChunk;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // The kernel configurations (ccsx_kernel.hip is compiled once per

@@ -26,7 +26,7 @@ EXPORTS = {
                    "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows",
                    "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault",
                    "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count",
-                   "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log"],
+                   "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
                     "ccsx_zmw_cost", "ccsx_partition",
@@ -65,6 +65,7 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_status_str.restype = C.c_char_p
         L.ccsx_gpu_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwIn), C.c_size_t, C.POINTER(ZmwOut)]
         L.ccsx_gpu_stage.argtypes = [C.c_void_p, C.POINTER(ZmwIn), C.c_size_t]
+        L.ccsx_gpu_stage_for.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwIn), C.c_size_t]
         L.ccsx_gpu_launch.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_float)]
         L.ccsx_gpu_fetch.argtypes = [C.c_void_p, C.POINTER(ZmwOut)]
         L.ccsx_gpu_staged_bytes.argtypes = [C.c_void_p]
@@ -303,9 +304,13 @@ class Engine:
             arr[i].nseg = len(lens)
         return arr, keep
 
-    def stage(self, zmws: list[Prepared]) -> None:
+    def stage(self, zmws: list[Prepared], mode: int | None = None) -> None:
+        """Stage a slice (tight capacities); with `mode`, the capacities
+        ccsx_gpu_run uses for that mode (ccsx_gpu_stage_for)."""
         arr, keep = self._build_in(zmws)
-        if self._L.ccsx_gpu_stage(self._ctx, arr, len(zmws)) != 0:
+        rc = (self._L.ccsx_gpu_stage(self._ctx, arr, len(zmws)) if mode is None
+              else self._L.ccsx_gpu_stage_for(self._ctx, mode, arr, len(zmws)))
+        if rc != 0:
             self._err("ccsx_gpu_stage")
         self._keep = (arr, keep)
         self._nz = len(zmws)

@@ -89,6 +89,11 @@ int ccsx_gpu_bp_log(const ccsx_ctx *ctx, size_t zmw, const uint32_t **pairs, uin
  * ccsx_gpu_launch returns the kernel time measured with HIP events on the
  * context's stream. */
 int ccsx_gpu_stage(ccsx_ctx *ctx, const ccsx_zmw_in *z, size_t nz);
+/* ccsx_gpu_stage with the tight capacities ccsx_gpu_run uses for `mode`
+ * (shredded: workspaces and the LDS read buffer sized for the pushed windows,
+ * not whole segments), so a staged slice runs the same kernel instance a
+ * ccsx_gpu_run slice would. */
+int ccsx_gpu_stage_for(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz);
 int ccsx_gpu_launch(ccsx_ctx *ctx, int mode, float *kernel_ms);
 int ccsx_gpu_fetch(ccsx_ctx *ctx, ccsx_zmw_out *out);
 

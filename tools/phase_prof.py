@@ -13,7 +13,7 @@ zs = [cx.prepare(cx.synth_zmw(20201104, h, a.L, a.passes)[0]) for h in range(a.n
 e = cx.Engine(0)
 if a.kcfg >= 0:
     e.set_kernel_cfg(a.kcfg)
-e.stage(zs)
+e.stage(zs, a.mode)
 e.launch(a.mode)
 e.set_profiling(True)
 ms = e.launch(a.mode)

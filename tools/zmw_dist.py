@@ -14,7 +14,7 @@ if a.nzmw:
     cfg["nzmw"] = a.nzmw
 zs = bench.make_batch(cfg, 0)
 e = cx.Engine(0)
-e.stage(zs)
+e.stage(zs, a.mode)
 plain = [e.launch(cfg["mode"]) for _ in range(3)]
 e.set_profiling(True)
 ms = e.launch(cfg["mode"])
