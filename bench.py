@@ -33,12 +33,15 @@ CONFIGS = {
               nzmw=1000, L=20000, passes=5, mode=1),
     "D": dict(workload="D: 10000 ZMWs x 2 kb insert x 30 passes, 10% error, shredded mode",
               nzmw=10000, L=2000, passes=30, mode=0),
-    # subreads beyond the LDS read buffer (100 kb): the HBM-read kernel
-    # instance (not a BASELINE config; 440 kb per ZMW stays under -M 500000)
-    "H": dict(workload="H: 256 ZMWs x 110 kb insert x 4 passes, 10% error, shredded mode (HBM-read kernel instance)",
-              nzmw=256, L=110000, passes=4, mode=0),
-    "HP": dict(workload="HP: 256 ZMWs x 110 kb insert x 4 passes, 10% error, primitive (-P) mode "
-                        "(HBM-read kernel instance)", nzmw=256, L=110000, passes=4, mode=1),
+    # subreads beyond the LDS read buffer (100 kb; not BASELINE configs, 440 kb
+    # per ZMW stays under -M 500000), 1,000 ZMWs like B and C so GCUPS compare
+    # at the same chip fill: -P pushes whole segments (the HBM-read kernel
+    # instance); shredded mode pushes 2-10 kb windows (the LDS instance with
+    # its 8,192-base tight-cap buffer)
+    "H": dict(workload="H: 1000 ZMWs x 110 kb insert x 4 passes, 10% error, shredded mode (long subreads)",
+              nzmw=1000, L=110000, passes=4, mode=0),
+    "HP": dict(workload="HP: 1000 ZMWs x 110 kb insert x 4 passes, 10% error, primitive (-P) mode "
+                        "(HBM-read kernel instance)", nzmw=1000, L=110000, passes=4, mode=1),
     # a per-GPU slice of config E (500k ZMWs, mixed 5-25 kb inserts, 5-12 passes)
     "E": dict(workload="E-slice: 2000 ZMWs per GPU, insert ~U[5,25] kb x passes ~U[5,12] (total <= 450 kb), "
                        "10% error, shredded mode", nzmw=2000, L=0, passes=0, mode=0),

@@ -180,6 +180,7 @@ struct ccsx_ctx {
     std::string err;
     Slot slot[2];
     int32_t cfg_force = -1;            // test hook: -1 = by slice size
+    uint32_t wg_cap = 0;               // measurement hook (CCSX_WG_PER_CU): LDS request padded to cap workgroups per CU
     uint32_t ncu = 256;                // compute units of the device
     uint64_t reruns = 0;               // ZMWs ccsx_gpu_run re-ran with full caps
     bool profiling = false;
@@ -238,6 +239,12 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
     if (const char *k = getenv("CCSX_KCFG")) {
         const int v = atoi(k);
         if (v >= -1 && v < ccsx::kCfgCount) c->cfg_force = v;
+    }
+    // CCSX_WG_PER_CU caps the resident workgroups per CU by padding the LDS
+    // request (the residency curve of DESIGN.md section 5; never the default)
+    if (const char *k = getenv("CCSX_WG_PER_CU")) {
+        const int v = atoi(k);
+        if (v > 0 && v <= 16) c->wg_cap = (uint32_t)v;
     }
     if (e != hipSuccess) {
         fprintf(stderr, "[ccsx_gpu] cannot open device %d: %s\n", device, hipGetErrorString(e));
@@ -511,7 +518,8 @@ static int launch_slot(ccsx_ctx *c, Slot &s, int mode)
         HIPCHK(c, s.d_prof.reserve(s.nz * ccsx::kProfSlots * 8));
         a.prof = s.d_prof.as<unsigned long long>();
     }
-    const uint32_t lds = kcfg_lds(s.cfg, s.lds_extra);
+    uint32_t lds = kcfg_lds(s.cfg, s.lds_extra);
+    if (c->wg_cap) lds = std::max<uint32_t>(lds, 160u * 1024u / (c->wg_cap + 1) + 1024u);
     if (lds > 160 * 1024) {
         c->err = "reads too long for the LDS read buffer";
         return -1;

@@ -77,8 +77,16 @@ def test_bench_two_ranks_on_device():
     small = ["--steps", "2", "--warmup", "1", "--nzmw", "96", "--e2e-zmws", "64", "--no-cpu-baseline"]
     one = _run_bench(1, small)
     two = _run_bench(2, small)
+    import ccsx_amd.native as nat
+    ndev = nat.device_count()
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
-    assert two["config"].get("ranks_per_device", 1) >= 1
+    assert "ranks_per_device" not in one["config"]
+    # two ranks on fewer than two visible GPUs share a device: the line must
+    # say so (a rehearsal, never a two-GPU number); on two or more, it must not
+    if ndev < 2:
+        assert two["config"]["ranks_per_device"] == 2
+    else:
+        assert "ranks_per_device" not in two["config"]
     # rank 1 aligns its own 96 holes: the summed cells are two ranks' worth,
     # and the two ranks' cell counts differ (disjoint synthetic holes)
     assert two["cells_per_step"] > one["cells_per_step"]

@@ -7,7 +7,10 @@ its output checked byte for byte against the oracle on the same ZMWs.
 The input is tools/synth_fa's config-E FASTA (insert ~U[5,25] kb x 5-12
 passes, 10 % error), written to a file first and fed on stdin (--pipe: the
 generator's stdout piped straight into the CLI, so the generator's own rate
-bounds the run).  Writes DIR/cli_stream.json and DIR/cli_stream_timing.log.
+bounds the run, and the CLI's output read from a FIFO by a thread that keeps
+only the sampled records: nothing touches the disk, so a 500k-ZMW run needs
+neither 65 GB of input nor 7.5 GB of output on the box).  Writes
+DIR/cli_stream.json and DIR/cli_stream_timing.log.
 Test infrastructure: the oracle is only the checker of the sample."""
 import argparse
 import json
@@ -16,6 +19,7 @@ import random
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -43,8 +47,32 @@ def main():
     gen = [GEN, str(a.n), str(a.hole0), "0", "0", str(a.jobs)]
     env = dict(os.environ, CCSX_TIMING="1")
     log = open(os.path.join(a.out, "cli_stream_timing.log"), "w")
+    # the sampled holes, drawn before the run (the FIFO reader keeps only them)
+    rnd = random.Random(a.hole0 ^ a.n)
+    sample = sorted(rnd.sample(range(a.hole0, a.hole0 + a.n), min(a.sample, a.n)))
+    want_holes = set(sample)
+    scan = {"got": {}, "nrec": 0, "in_order": True, "bytes": 0}
+
+    def read_output(path):
+        got, nrec, in_order, last, cur, nb = {}, 0, True, -1, None, 0
+        with open(path, "rb") as f:
+            for line in f:
+                nb += len(line)
+                if line.startswith(b">"):
+                    nrec += 1
+                    h = int(line.split(b"/")[1])
+                    in_order &= h > last
+                    last = h
+                    cur = h if h in want_holes else None
+                elif cur is not None:
+                    got[cur] = line.rstrip(b"\n")
+        scan.update(got=got, nrec=nrec, in_order=in_order, bytes=nb)
+
     try:
         if a.pipe:
+            os.mkfifo(ccs)
+            rd = threading.Thread(target=read_output, args=(ccs,))
+            rd.start()
             t0 = time.perf_counter()
             g = subprocess.Popen(gen, stdout=subprocess.PIPE)
             r = subprocess.run([BIN, "-A", "-j", str(a.jobs), "-", ccs], stdin=g.stdout, stderr=log, env=env)
@@ -52,6 +80,14 @@ def main():
             g.wait()
             res["cli_s"] = time.perf_counter() - t0
             res["input_bytes"] = None
+            if r.returncode != 0:
+                # unblock the reader if the CLI never opened its output (no
+                # reader left: ENXIO, nothing to unblock)
+                try:
+                    os.close(os.open(ccs, os.O_WRONLY | os.O_NONBLOCK))
+                except OSError:
+                    pass
+            rd.join()
         else:
             t0 = time.perf_counter()
             with open(fa, "wb") as f:
@@ -69,24 +105,12 @@ def main():
         res["zmws_per_s"] = a.n / res["cli_s"]
         print(f"cli: {a.n} ZMWs in {res['cli_s']:.2f} s = {res['zmws_per_s']:.0f} ZMWs/s", flush=True)
         # the output: one record per ZMW with a CCS, in input (hole) order
-        rnd = random.Random(a.hole0 ^ a.n)
-        sample = sorted(rnd.sample(range(a.hole0, a.hole0 + a.n), min(a.sample, a.n)))
-        want_holes = set(sample)
-        got, nrec, holes_in_order = {}, 0, True
-        last = -1
-        with open(ccs, "rb") as f:
-            for line in f:
-                if line.startswith(b">"):
-                    nrec += 1
-                    h = int(line.split(b"/")[1])
-                    holes_in_order &= h > last
-                    last = h
-                    cur = h if h in want_holes else None
-                elif cur is not None:
-                    got[cur] = line.rstrip(b"\n")
-        res["records"] = nrec
-        res["records_in_input_order"] = holes_in_order
-        res["output_bytes"] = os.path.getsize(ccs)
+        if not a.pipe:
+            read_output(ccs)
+        got = scan["got"]
+        res["records"] = scan["nrec"]
+        res["records_in_input_order"] = scan["in_order"]
+        res["output_bytes"] = scan["bytes"]
         # the oracle on the sample's push lists
         import bench
         import ccsx_amd as cx

@@ -17,7 +17,8 @@
 #   cli:N[:pipe]       CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py)
 #   env:NAME=VALUE     export NAME for the following steps (env:NAME= unsets it)
 #   lib:NAME           the following steps load ccsx_amd/NAME (CCSX_LIB); lib: resets
-# Environment: CCSX_LIB selects a library variant for the bench steps.
+# Environment: CCSX_LIB selects a library variant for the bench steps; CCSX_WG_PER_CU caps the
+# resident workgroups per CU (LDS request padding, a measurement hook).
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -47,7 +48,7 @@ step() {
         timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" && cat "$OUT/bench.json"
         return $?
       fi
-      local f="$OUT/bench_${cfg}${k:+_k$k}${CCSX_LIB:+_${CCSX_LIB%.so}}.json"
+      local f="$OUT/bench_${cfg}${k:+_k$k}${CCSX_LIB:+_${CCSX_LIB%.so}}${CCSX_WG_PER_CU:+_w$CCSX_WG_PER_CU}.json"
       timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$k") > "$f" 2> "${f%.json}.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['value'], 'ZMWs/s', d['gcups'], 'GCUPS', 'cfg', d['roofline'].get('kernel_cfg'))" "$f" ;;
     ab)  # ab:CFG:KCFG[,KCFG...][:LIB,LIB...] -- 3 interleaved rounds over kernel cfgs x libraries
