@@ -231,7 +231,7 @@ def main():
     ap.add_argument("--nzmw", type=int, default=0, help="override ZMWs per GPU (testing only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-zmws", type=int, default=16384, help="ZMWs per GPU of the end-to-end line (0: skip)")
-    ap.add_argument("--kcfg", type=int, default=-1, help="force a kernel configuration (0 latency, 1 occupancy, "
+    ap.add_argument("--kcfg", type=int, default=-1, help="force a kernel configuration (0 latency, 1 occupancy, 3 solo, "
                                                          "2 throughput; -1: by slice size)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])

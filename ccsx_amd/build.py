@@ -30,14 +30,17 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 
 ARCH = os.environ.get("CCSX_OFFLOAD_ARCH", "gfx950")
 # the kernel configurations (ccsx_layout.h KernelCfg): latency (8-row DP
-# blocks, 32-row ring), occupancy (4-row blocks, 24-row ring) and throughput
-# (two-wave workgroups)
+# blocks, 32-row ring), occupancy (4-row blocks, 24-row ring), throughput
+# (two-wave workgroups) and solo (one-wave workgroups)
 KCFGS = [(n, [f"-DCCSX_KCFG={n}", f"-DCCSX_LAUNCH=ccsx_launch_zmw_{n}", f"-DCCSX_INFO=ccsx_kcfg_info_{n}"] + d)
          for n, d in [("lat", ["-DCCSX_RINGA=32", "-DCCSX_BLK=8"]),
                       ("occ", ["-DCCSX_RINGA=24", "-DCCSX_BLK=4"]),
                       # two-wave workgroups, a 16-row ring read back 8 rows
                       # no issue priorities: two wave 0s share each SIMD (A/B r03g: D 567 -> 550 ms)
                       ("tput", ["-DCCSX_RINGA=16", "-DCCSX_BLK=4", "-DCCSX_RING=8", "-DCCSX_HELPERS=1",
+                                "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0"]),
+                      # one-wave workgroups (dp_solo), an 8-row ring, one traceback buffer
+                      ("solo", ["-DCCSX_RINGA=8", "-DCCSX_BLK=4", "-DCCSX_RING=8", "-DCCSX_HELPERS=0",
                                 "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0"])]]
 
 

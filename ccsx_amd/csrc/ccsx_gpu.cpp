@@ -25,20 +25,24 @@
 extern "C" hipError_t ccsx_launch_zmw_lat(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" hipError_t ccsx_launch_zmw_occ(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" hipError_t ccsx_launch_zmw_tput(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+extern "C" hipError_t ccsx_launch_zmw_solo(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" void ccsx_kcfg_info_lat(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_occ(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_tput(ccsx::KCfgInfo *o);
+extern "C" void ccsx_kcfg_info_solo(ccsx::KCfgInfo *o);
 
 namespace {
 typedef hipError_t (*LaunchFn)(const ccsx::KArgs *, uint32_t, hipStream_t);
-constexpr LaunchFn kLaunch[ccsx::kCfgCount] = {ccsx_launch_zmw_lat, ccsx_launch_zmw_occ, ccsx_launch_zmw_tput};
+constexpr LaunchFn kLaunch[ccsx::kCfgCount] = {ccsx_launch_zmw_lat, ccsx_launch_zmw_occ, ccsx_launch_zmw_tput,
+                                               ccsx_launch_zmw_solo};
 
 ccsx::KCfgInfo kcfg_info(int cfg)
 {
     ccsx::KCfgInfo o{};
     if (cfg == ccsx::kCfgLatency) ccsx_kcfg_info_lat(&o);
     else if (cfg == ccsx::kCfgOccupancy) ccsx_kcfg_info_occ(&o);
-    else ccsx_kcfg_info_tput(&o);
+    else if (cfg == ccsx::kCfgThroughput) ccsx_kcfg_info_tput(&o);
+    else ccsx_kcfg_info_solo(&o);
     return o;
 }
 
@@ -301,8 +305,8 @@ constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
 // LDS read buffer of a tight-cap shredded slice (bases)
 constexpr uint32_t kShredReadCap = 8192;
 // slices of at least this many times the occupancy configuration's resident
-// workgroups run the throughput configuration
-constexpr size_t kTputSliceFactor = 3;
+// workgroups run the solo configuration
+constexpr size_t kSoloSliceFactor = 3;
 
 // launch classes of ccsx_gpu_run's slices: LDS read buffer up to 32 kb (4+
 // workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never
@@ -415,17 +419,19 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
     // the cursors, or the HBM-read instance's read window
     s.lds_extra = s.lds_read_words ? s.lds_read_words + s.lds_nmax : ccsx::kRdWinBytes / 4;
     // kernel configuration (ccsx_layout.h KernelCfg): the latency one if it
-    // keeps the whole slice resident; the throughput one (two-wave
-    // workgroups) once the slice is several times what the occupancy one
-    // keeps resident, so the launch is bound by resident ZMWs rather than by
-    // its slowest ZMW's chain (which is ~27 % longer there); the occupancy
-    // one in between
+    // keeps the whole slice resident; the solo one (one-wave workgroups, ~3x
+    // the resident ZMWs) once the slice is several times what the occupancy
+    // one keeps resident, so the launch is bound by resident ZMWs rather than
+    // by its slowest ZMW's chain (which is ~44 % longer there: config D 316
+    // GCUPS solo vs 245 two-wave vs 213 occupancy, config B 74 vs 52 ms;
+    // profiles/r03/r03n_*); the occupancy one in between.  (The two-wave
+    // throughput configuration is only chosen by ccsx_gpu_set_kernel_cfg.)
     {
         const uint32_t extra = s.lds_extra;
         const size_t res_lat = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgLatency, extra);
         const size_t res_occ = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgOccupancy, extra);
-        s.cfg = nz <= res_lat ? ccsx::kCfgLatency : nz < kTputSliceFactor * res_occ ? ccsx::kCfgOccupancy
-                                                                                  : ccsx::kCfgThroughput;
+        s.cfg = nz <= res_lat ? ccsx::kCfgLatency : nz < kSoloSliceFactor * res_occ ? ccsx::kCfgOccupancy
+                                                                                  : ccsx::kCfgSolo;
         if (c->cfg_force >= 0) s.cfg = c->cfg_force;
     }
     size_t freeb = 0, totb = 0;

@@ -18,7 +18,11 @@
 // HBM, 256 B per row, rotated per row for the traceback's LDS banks.
 // Traceback (SPEC.md §4) walks those records on wave 0 from 32-row blocks
 // LDS-DMA'd double-buffered; merge (§5) and the column counts (§6) run on all
-// three waves.
+// three waves.  The same source builds four configurations (ccsx_layout.h
+// KernelCfg): three-wave latency / occupancy ones, a two-wave throughput one
+// (one helper) and a one-wave solo one (dp_solo: the wave computes the
+// decision bits itself, an 8-row ring, one traceback buffer; ~15 ZMWs per CU
+// for slices of many thousands of ZMWs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,19 +44,9 @@
 namespace ccsx {
 namespace CCSX_KCFG {
 
-// CCSX_PEX_RING (the one-helper throughput configuration): wave 0 hands each
-// row's insertion prefix max (Pex, one word per lane) to the helper through
-// a small LDS ring instead of the helper re-running the 7-step DPP scan --
-// the helper, not wave 0, is that configuration's slower chain.  The ring
-// holds the helper's lag: two lockstep blocks.
-#ifndef CCSX_PEX_RING
-#define CCSX_PEX_RING 0
-#endif
 #ifndef CCSX_BLK
 #define CCSX_BLK 8
 #endif
-constexpr int kPexRing = CCSX_PEX_RING;
-constexpr int kPexRows = 2 * CCSX_BLK;
 
 constexpr int kO = -3, kE = -2, kMs = 2, kXs = -6;  // main.c:842-847
 enum { HC_MPRED = 0, HC_MSRC = 1, HC_DEL = 2, HC_INS = 3 };
@@ -337,8 +331,7 @@ constexpr int kLdsRing = 0;                              // kRingA DP rows x kRo
 constexpr int kLdsDiag = kLdsRing + kRingA * kRowW;      // 32: helpers' diagnostic counters at exit
 constexpr int kLdsOffRing = kLdsDiag + 32;               // 64: band offset of DP row q at q & 63
 constexpr int kLdsJob = kLdsOffRing + 64;                // 16: DP job / results
-constexpr int kLdsPex = kLdsJob + 16;                    // kPexRing: kPexRows rows x 64 lanes of Pex
-constexpr int kLdsFixed = kLdsPex + kPexRing * kPexRows * 64;  // then: the read (nibble pairs), shredding cursors
+constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
 
 // per lane: row r0+lane's info and first four predecessors
@@ -400,15 +393,17 @@ __device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; 
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
 constexpr int kBlkAB = CCSX_BLK;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2, ...
-// helper waves per workgroup: 2 (latency / occupancy configurations) or 1
-// (throughput configuration: two-wave workgroups, twice the resident ZMWs)
+// helper waves per workgroup: 2 (latency / occupancy configurations), 1
+// (throughput configuration: two-wave workgroups, twice the resident ZMWs) or
+// 0 (solo configuration: one wave computes the decision bits too, dp_solo)
 #ifndef CCSX_HELPERS
 #define CCSX_HELPERS 2
 #endif
 constexpr int kHelpers = CCSX_HELPERS;
-static_assert(kHelpers == 1 || kHelpers == 2, "one or two helper waves");
+static_assert(kHelpers >= 0 && kHelpers <= 2, "zero, one or two helper waves");
 constexpr int kBlockThreads = 64 * (1 + kHelpers);
-static_assert(kBlkAB % kHelpers == 0, "each helper takes the same number of rows per block");
+constexpr int kHelperStep = kHelpers ? kHelpers : 1;
+static_assert(kBlkAB % kHelperStep == 0, "each helper takes the same number of rows per block");
 // issue priorities (s_setprio): wave 0 always, helpers during merge; helpers
 // run their DP decision bits at the default 0
 #ifndef CCSX_PRIO_WAVE0
@@ -418,7 +413,7 @@ static_assert(kBlkAB % kHelpers == 0, "each helper takes the same number of rows
 #define CCSX_PRIO_MERGE 2
 #endif
 constexpr int kPrioWave0 = CCSX_PRIO_WAVE0, kPrioMerge = CCSX_PRIO_MERGE;
-static_assert(kRingA >= kRing + 2 * kBlkAB, "B reads predecessors up to kRing rows behind its row");
+static_assert(kRingA >= kRing + (kHelpers ? 2 * kBlkAB : 0), "B reads predecessors up to kRing rows behind its row");
 
 
 enum JobKind : int32_t { kJobExit = 0, kJobDp = 1, kJobMerge = 2, kJobColumns = 3 };
@@ -690,22 +685,23 @@ __device__ __forceinline__ LaneK lane_consts(int lane)
 }
 
 // wave 0, the rows that are not "chain, band moved by 1": chain rows moved
-// by 0 or 2 (DPP) and general rows (predecessors from the ring)
+// by 0 or 2 (DPP) and general rows (predecessors from the ring).  SLOTS
+// (the solo configuration, which computes its own decision bits): A also
+// carries the predecessor tags and D-ext bits, as the helpers' dpB_cold does.
+template <bool SLOTS>
 __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r, uint32_t info, int32_t coff,
-                                         int32_t lim, int32_t &off_o, int32_t &Mh0, int32_t &Mh1, int32_t &Dv0,
-                                         int32_t &Dv1, int &kind)
+                                         int32_t lim, int32_t &off_o, PredAcc &A, int &kind)
 {
     const int lane = lane_id();
     const int li = (int)(r & 63u);
     const uint32_t np = info >> 8;
     const int32_t sh = coff - S.pOff;
     const int32_t *ring = z.lds + kLdsRing;
-    PredAcc A;
     int32_t off;
     kind = 4;
     if (info & kInfoFar) {
         kind = 0;
-        far_terms<false>(z, r, np, S.vOff, S.vKey, lim, true, off, A);
+        far_terms<SLOTS>(z, r, np, S.vOff, S.vKey, lim, true, off, A);
     } else if ((info & kInfoChain) && (uint32_t)sh <= 2u) {
         kind = 1;
         // chain row, band moved by 0..2 (1: a spill row)
@@ -719,14 +715,14 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
             hA = S.H1, hB = wave_shl1(kNegH, S.H0), hC = wave_shl1(kNegH, S.H1);
             dB = wave_shl1(kNeg, S.D0), dC = wave_shl1(kNeg, S.D1);
         }
-        pred_fold<false>(A, 0, 0, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, 0, 1u, hA, hB, hC, dB, dC);  // the predecessor is row r - 1
     } else if (np == 1) {
         kind = 2;
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
         const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
         off = min(max(o0 + 127 - (k0 & 127) + 1 - kW / 2, 0), lim);
-        pred_terms_n<1, false>(ring, r, off, p0, p0, o0, o0, lane, A);
+        pred_terms_n<1, SLOTS>(ring, r, off, p0, p0, o0, o0, lane, A);
     } else if (np == 2) {
         kind = 3;
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
@@ -739,7 +735,7 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
         const bool second = (k1 >> 7) > (k0 >> 7);
         const int32_t ko = second ? k1 : k0, oo = second ? o1 : o0;
         off = min(max(oo + 127 - (ko & 127) + 1 - kW / 2, 0), lim);
-        pred_terms_n<2, false>(ring, r, off, p0, p1, o0, o1, lane, A);
+        pred_terms_n<2, SLOTS>(ring, r, off, p0, p1, o0, o1, lane, A);
     } else {
         const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
         const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
@@ -761,9 +757,9 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
             if (np > 3 && (k3 >> 7) > bm) bm = k3 >> 7, barg = o3 + 127 - (k3 & 127);
             off = min(max(barg + 1 - kW / 2, 0), lim);
         }
-        pred_terms<false>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
+        pred_terms<SLOTS>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
     }
-    off_o = off, Mh0 = A.Mh0, Mh1 = A.Mh1, Dv0 = A.Dv0, Dv1 = A.Dv1;
+    off_o = off;
 }
 
 // wave 0: one DP row (SPEC.md §3.1-§3.4 values).  FULL: m >= W, every band
@@ -830,7 +826,6 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
-        if (kPexRing) z.lds[kLdsPex + (r % kPexRows) * 64 + lane] = Pex;  // for the helper (dpB_tail)
         // (inline asm measured 0.6 % faster than the compiler's writelane
         // intrinsic here: it keeps vOff / vKey out of the scheduler's way)
         S.vOff = writelane(S.vOff, off, li);
@@ -900,9 +895,11 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
             tail(coff, qp, S.H0, S.H1, Dv0, Dv1, false);
         }
     } else {
-        int32_t off, Mh0, Mh1, Dv0, Dv1;
+        int32_t off;
+        PredAcc A;
         int kind;
-        dpA_cold(z, S, r, info, coff, lim, off, Mh0, Mh1, Dv0, Dv1, kind);
+        dpA_cold<false>(z, S, r, info, coff, lim, off, A, kind);
+        const int32_t Mh0 = A.Mh0, Mh1 = A.Mh1, Dv0 = A.Dv0, Dv1 = A.Dv1;
 #ifdef CCSX_DP_STAMPS
         if (info & kInfoSpill) kind = 5;
         ckind = kind;
@@ -1003,8 +1000,7 @@ __device__ __forceinline__ void dpB_tail(Z &z, BState &S, uint32_t r, uint32_t m
     const int32_t hp0 = max(M0, A.Dv0), hp1 = max(M1, A.Dv1);
     // insertions (SPEC.md §3.4): the same prefix-max scan as wave 0's
     const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
-    const int32_t Pex = kPexRing ? z.lds[kLdsPex + (r % kPexRows) * 64 + lane]
-                                 : wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
+    const int32_t Pex = wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
     const int32_t X1L = wave_shr1(INT32_MAX, X1);
     const int32_t ex1 = max(Pex, X0);
     const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
@@ -1097,7 +1093,7 @@ __device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t
     const LaneK c = lane_consts(lane);
     recwin_begin(z, S.W, r0);
 #pragma unroll
-    for (uint32_t i = h; i < (uint32_t)kBlkAB; i += kHelpers)
+    for (uint32_t i = h; i < (uint32_t)kBlkAB; i += kHelperStep)
         if (r0 + i < R) dpB_row<FULL>(z, S, r0 + i, m, lim, vOff, c);
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
     if (h == 0 && ((r0 & 15u) == 16u - kBlkAB || rend == R)) {
@@ -1222,6 +1218,232 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
     }
 }
 
+// ----------------------------------------------------------------------------
+// The solo configuration (kHelpers == 0): one wave per ZMW.  For slices of
+// many thousands of ZMWs the launch is bound by how many ZMW chains each SIMD
+// holds, not by one chain's latency (config D: 150 / 200 / 222 / 244 GCUPS
+// at 4 / 6 / 7 / 8 two-wave workgroups per CU, profiles/r03/r03m_*).  A
+// one-wave workgroup needs 16 waves' registers per CU for 16 ZMWs and, with
+// no helper lagging behind, a ring of only kRing rows (8: 8.7 KB), so about
+// 15 ZMWs are resident per CU instead of 8.  The wave computes each row's
+// decision bits itself, from the values it already holds (the helpers
+// recompute them from the ring): the cell codes, D-ext / I-ext, predecessor
+// tags, the free-end candidates and the record store of dpB_tail, bit for
+// bit the same records.
+// ----------------------------------------------------------------------------
+struct SolB {
+    int32_t bE;       // best free-end value of this lane's cells
+    uint32_t bKey;    // its row * 2 + cell
+    int32_t bOff;     // its row's band offset
+    __amdgpu_buffer_rsrc_t rc;  // cell records of this DP (R rows x 256 B)
+};
+
+template <bool FULL>
+__device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, int32_t lim, uint32_t m, const LaneK &c,
+                                        uint32_t ring)
+{
+    const int lane = lane_id();
+    const int li = (int)(r & 63u);
+    const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
+    const uint32_t base = info & 3u;
+    const uint32_t np = info >> 8;
+    const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
+    const int32_t pb = S.pOff & ~1;  // S.qn: read bytes (pOff >> 1) + lane, + 1
+    const int32_t sh = coff - S.pOff;
+    const uint32_t fast = (uint32_t)(S.fmask >> li) & ((uint32_t)sh <= 1u ? 1u : 0u);
+    PredAcc A;
+    int32_t off;
+    uint32_t qp;
+    bool cold;
+    if (__builtin_expect(fast, 1)) {
+        // the only predecessor is row r - 1 (tag 1), band moved by 0 or 1:
+        // its cells from registers by DPP; D-ext = the D term won strictly
+        cold = false;
+        off = coff;
+        qp = S.qn >> (4u * (uint32_t)(coff - pb));
+        A.ms0 = A.ms1 = A.ds0 = A.ds1 = 1u;
+        int32_t a0, b0, a1, b1;
+        if (sh == 0) {
+            A.Mh0 = wave_shr1(kNegH, S.H1), A.Mh1 = S.H0;
+            a0 = S.H0 + (kO + kE), b0 = S.D0 + kE, a1 = S.H1 + (kO + kE), b1 = S.D1 + kE;
+        } else {
+            A.Mh0 = S.H0, A.Mh1 = S.H1;
+            a0 = S.H1 + (kO + kE), b0 = S.D1 + kE;
+            a1 = wave_shl1(kNegH, S.H0) + (kO + kE), b1 = wave_shl1(kNeg, S.D0) + kE;
+        }
+        A.Dv0 = max(a0, b0), A.Dv1 = max(a1, b1);
+        A.dx0 = b0 > a0 ? 4u : 0u, A.dx1 = b1 > a1 ? 4u : 0u;
+    } else {
+        cold = true;
+        int kind;
+        dpA_cold<true>(z, S, r, info, coff, lim, off, A, kind);
+        (void)kind;
+        const uint32_t d = (uint32_t)(off - pb);
+        qp = d <= 3u ? S.qn >> (4u * d) : rd_byte(z, off, 0, z.hbm && win_has(z.wa, 2, off)) >> ((uint32_t)(off & 1) * 4u);
+    }
+    // the next row's read window, a row ahead of its use
+    {
+        const bool w = z.hbm && win_has(z.wa, 2, off);
+        S.qn = rd_byte(z, off, 0, w) | rd_byte(z, off, 1, w) << 8;
+    }
+    // the recurrence (dpA_row's tail) and the decision bits (dpB_tail's) from
+    // the same values
+    const int32_t srcu = c.src0 + kE * off;
+    const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
+    const bool mp0 = A.Mh0 >= src0, mp1 = A.Mh1 >= srcu + kE;
+    const int32_t M0 = max(A.Mh0, src0) + ((qp & 3u) == base ? kMs : kXs);
+    const int32_t M1 = max(A.Mh1, srcu + kE) + (((qp >> 2) & 3u) == base ? kMs : kXs);
+    int32_t Dv0 = A.Dv0, Dv1 = A.Dv1;
+    const bool d0 = Dv0 > M0, d1 = Dv1 > M1;
+    const int32_t hp0 = max(M0, Dv0), hp1 = max(M1, Dv1);
+    const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
+    int32_t incl = max(X0, X1);
+    int32_t rk0 = (hp0 << 7) | c.kc0, rk1 = (hp1 << 7) | c.kc1;
+    if (!FULL) {
+        if ((uint32_t)c.L2 >= m) rk0 = INT32_MIN, Dv0 = kNeg;
+        if ((uint32_t)c.L2 + 1 >= m) rk1 = INT32_MIN, Dv1 = kNeg;
+    }
+    int32_t rk = max(rk0, rk1);
+    wave_incl_max2(incl, rk);
+    const int32_t Pex = wave_shr1(kNeg, incl);
+    const int32_t ex1 = max(Pex, X0);
+    int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(ex1 + c.cI1, hp1);
+    if (!FULL) {
+        if ((uint32_t)c.L2 >= m) nH0 = kNegH;
+        if ((uint32_t)c.L2 + 1 >= m) nH1 = kNegH;
+    }
+    const int32_t key = __builtin_amdgcn_readlane(rk, 63);
+    int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
+    row[0] = make_int2(nH0, nH1);
+    row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
+    S.vOff = writelane(S.vOff, off, li);
+    S.vKey = writelane(S.vKey, key, li);
+    if (cold && (info & kInfoSpill)) {
+        // a successor lies beyond the ring: keep this row in HBM
+        const uint32_t sl = S.nspill++;
+        if (sl < z.d.scap) {
+            int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)sl * kSpillRec);
+            reinterpret_cast<int2 *>(rec)[lane] = make_int2(nH0, nH1);
+            reinterpret_cast<int2 *>(rec + kW)[lane] = make_int2(Dv0, Dv1);
+            if (lane == 0) rec[256] = off, rec[257] = key, P<uint32_t>(z, z.L.sslot)[r] = sl;
+        } else {
+            z.status = kErrSpill;
+        }
+    }
+    S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
+    S.pOff = off;
+    S.pArg = off + 127 - (key & 127);
+    // decision bits (SPEC.md §3.4): code, D-ext, I-ext, M / D tags
+    const int32_t X1L = wave_shr1(INT32_MAX, X1);
+    const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
+    const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
+    const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
+    const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
+    uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
+    uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
+    if (__builtin_expect(np > 63u, 0)) {
+        // wide slot record of row r: u16 M / D slots per cell
+        reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
+            make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
+    }
+    // free-end candidates (SPEC.md §3.5) on H'
+    const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
+    int32_t e0 = X0 + eb;
+    int32_t e1 = X1 + eb;
+    if (FULL) {
+        e1 += (off == lim && lane == 63) ? 3 : 0;
+    } else {
+        if ((uint32_t)c.L2 == m - 1) e0 += 3;
+        if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
+        if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
+        if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
+    }
+    if (e0 > B.bE) B.bE = e0, B.bKey = r * 2, B.bOff = off;
+    if (e1 > B.bE) B.bE = e1, B.bKey = r * 2 + 1, B.bOff = off;
+    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), B.rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
+                                          0);
+}
+
+// rows [r0, r0 + kBlkAB) and, per 16-row group, the row meta words {band
+// offset | far << 31} the traceback reads (helper 0's job in dpB_block)
+template <bool FULL>
+__device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0, uint32_t m)
+{
+    const int lane = lane_id();
+    const uint32_t R = z.R;
+    const int32_t lim = FULL ? (int32_t)m - kW : 0;
+    const LaneK c = lane_consts(lane);
+    recwin_begin(z, S.W, r0);
+    if ((r0 & 63u) == 0) {
+        const uint32_t inf = S.W.cur.info;
+        S.fmask = ballot((inf & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain);
+    }
+    static_assert(kRingA % kBlkAB == 0, "a block's rows occupy consecutive ring slots");
+    const uint32_t rb = (r0 % (uint32_t)kRingA) * (uint32_t)kRowW;
+    if (r0 + kBlkAB <= R) {
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i) dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + i * kRowW);
+    } else {
+        for (uint32_t i = 0; r0 + i < R; ++i) dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + i * kRowW);
+    }
+    const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
+    if ((r0 & 15u) == 16u - kBlkAB || rend == R) {
+        const uint32_t g0 = r0 & ~15u;
+        const uint32_t far = (S.W.cur.info & kInfoFar) ? 0x80000000u : 0u;
+        const auto rm = brsrc(reinterpret_cast<uint32_t *>(z.ws + z.L.rmeta) + g0, (rend - g0) * 4);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)S.vOff | far, rm, (uint32_t)(lane - (int)(g0 & 63u)) * 4u, 0, 0);
+    }
+    recwin_end(S.W, r0);
+}
+
+template <bool FULL>
+__device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
+{
+    const int lane = lane_id();
+    for (int i = lane; i < kRingA * 16; i += 64) {
+        const int k = i & 15;
+        const int w = k < 4 ? k : k < 8 ? kHc + kW + (k - 4) : k < 12 ? kDc - 4 + (k - 8) : kDc + kW + (k - 12);
+        z.lds[kLdsRing + (i >> 4) * kRowW + w] = k < 8 ? kNegH : kNeg;
+    }
+    if (z.hbm) {  // the read's first two window chunks
+        z.wa = 0, z.wpend = false;
+        win_load(z, 0);
+        win_load(z, 1);
+    }
+    AState S;
+    S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
+    S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
+    S.qn = rd_byte(z, 0, 0, true) | rd_byte(z, 0, 1, true) << 8;
+    S.nspill = 0;
+    S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
+    S.W.nxt = S.W.cur;
+    SolB B;
+    B.bE = INT32_MIN, B.bKey = 0, B.bOff = 0;
+    B.rc = brsrc(z.ws + z.L.codes, z.R * 256u);
+    const uint32_t nblk = dp_nblk(z.R);
+    for (uint32_t b = 0; b < nblk && !z.status; ++b) {
+        if (z.hbm && z.wpend) {
+            win_load(z, z.wa + 1);
+            z.wpend = false;
+        }
+        dpS_block<FULL>(z, S, B, b * kBlkAB, m);
+        if (z.hbm) {  // the block's last band entered the upper chunk: slide
+            z.wpend = (uint32_t)S.pOff >= (z.wa + 1) * kWinChunk;
+            z.wa += z.wpend ? 1u : 0u;
+        }
+    }
+    // the candidate: lexicographic (max score, min row, min j)
+    const int32_t best = wave_max(B.bE);
+    const uint32_t rsel = B.bE == best ? B.bKey >> 1 : 0x7FFFFFFFu;
+    const int32_t rmin = wave_min((int32_t)rsel);
+    const bool mine = B.bE == best && (B.bKey >> 1) == (uint32_t)rmin;
+    const int32_t jsel = mine ? B.bOff + 2 * lane + (int32_t)(B.bKey & 1u) : INT32_MAX;
+    er_out = best == INT32_MIN ? 0xFFFFFFFFu : (uint32_t)rmin;
+    ej_out = (uint32_t)wave_min(jsel);
+    wsync();  // records and row meta in HBM before the traceback's DMA reads them
+    z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
+}
+
 template <bool LM>
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid);
 __device__ __forceinline__ void columns_count(const Z &z, uint32_t n, uint32_t ncols, uint32_t tid, uint32_t T);
@@ -1292,8 +1514,13 @@ __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uin
         return;
     }
     z.pf[kPfTwRows] += z.R;
-    if (m >= (uint32_t)kW) dp_two_wave<true>(z, m, er_out, ej_out);
-    else dp_two_wave<false>(z, m, er_out, ej_out);
+    if (kHelpers == 0) {
+        if (m >= (uint32_t)kW) dp_solo<true>(z, m, er_out, ej_out);
+        else dp_solo<false>(z, m, er_out, ej_out);
+    } else {
+        if (m >= (uint32_t)kW) dp_two_wave<true>(z, m, er_out, ej_out);
+        else dp_two_wave<false>(z, m, er_out, ej_out);
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1306,6 +1533,12 @@ __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uin
 // ----------------------------------------------------------------------------
 constexpr uint32_t kTbRows = 32;
 constexpr uint32_t kTbBufWords = kTbRows * 64;  // 32 rows x 256 B
+// record blocks staged at once: two (the next block's DMA overlaps the walk
+// of the current one) where the DP ring area holds them, else one (the solo
+// configuration's 8-row ring: a block switch waits for its DMA, which the
+// other ZMWs resident on the SIMD cover)
+constexpr uint32_t kTbBufs = (uint32_t)(kRingA * kRowW) >= 2 * kTbBufWords + 128 ? 2u : 1u;
+constexpr uint32_t kTbMeta = kTbBufs * kTbBufWords;  // LDS word of the blocks' row meta (64 words per buffer)
 
 // Traceback step tables indexed by (state, cell code), state 0 = H, 1 = D,
 // 2 = I; code = hcode | D-ext << 2 | I-ext << 3 (SPEC.md §3.4, §4).
@@ -1331,7 +1564,7 @@ constexpr uint64_t tb_table(uint32_t st, bool act)
 }
 constexpr uint64_t kTbAct[3] = {tb_table(0, true), tb_table(1, true), tb_table(2, true)};
 constexpr uint64_t kTbNext[3] = {tb_table(0, false), tb_table(1, false), tb_table(2, false)};
-static_assert(2 * kTbBufWords + 128 <= kRingA * kRowW, "traceback buffers live in the DP ring area");
+static_assert(kTbBufs * (kTbBufWords + 64) <= (uint32_t)(kRingA * kRowW), "traceback buffers live in the DP ring area");
 
 // LDS-DMA of 32-row block bi into buffer buf: records (8 KB) and the row
 // meta words (band offset | far << 31); the data bypass VGPRs, so nothing in
@@ -1345,7 +1578,7 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
     for (int k = 0; k < 8; ++k)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(src + k * 1024), dst + k * 256, 16, 0, 0);
     const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + bi * kTbRows + lane;
-    __builtin_amdgcn_global_load_lds(ms, z.lds + 2 * kTbBufWords + buf * 64, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds(ms, z.lds + kTbMeta + buf * 64, 4, 0, 0);
 }
 
 // Plain MPRED steps k..3 of an aligned 4-column record window (traceback;
@@ -1470,7 +1703,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     uint32_t wnx = 0;
     int32_t jwn = INT32_MAX;
     auto enter = [&]() {
-        const uint32_t mt = (uint32_t)z.lds[2 * kTbBufWords + buf * 64 + lane];
+        const uint32_t mt = (uint32_t)z.lds[kTbMeta + buf * 64 + lane];
         voff = mt & 0x7FFFFFFFu;
         vrot = (tb_rot(lane) - 2u * voff) & 255u;
         farm = (uint32_t)ballot((mt >> 31) != 0u);
@@ -1483,7 +1716,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     tb_dma(z, bi, buf);
     __builtin_amdgcn_s_waitcnt(0);
     enter();
-    if (bi) tb_dma(z, bi - 1, buf ^ 1u);
+    if (kTbBufs == 2 && bi) tb_dma(z, bi - 1, buf ^ 1u);
     const auto rev = brsrc(ev, m * 4);
     uint32_t vev = 0;                      // events of bases [chunk, chunk + 64), lane = base & 63
     int32_t chunk = j & ~63;
@@ -1517,13 +1750,20 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         const unsigned long long ts0 = stamp();
 #endif
         const uint32_t nb = r / kTbRows;
-        if (nb + 1 != bi) {
+        if (kTbBufs == 1) {
+            // one buffer: the walk's LDS reads of the old block complete,
+            // then the new block's DMA
             __builtin_amdgcn_s_waitcnt(0);
-            tb_dma(z, nb, buf ^ 1u);  // not the prefetched neighbour
+            tb_dma(z, nb, 0u);
+        } else {
+            if (nb + 1 != bi) {
+                __builtin_amdgcn_s_waitcnt(0);
+                tb_dma(z, nb, buf ^ 1u);  // not the prefetched neighbour
+            }
+            buf ^= 1u;
         }
         bi = nb;
         base = bi * kTbRows;
-        buf ^= 1u;
         __builtin_amdgcn_s_waitcnt(0);
         enter();
         if (pend >= 0) {
@@ -1531,7 +1771,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                                                   0, 0);
             pend = -1;
         }
-        if (bi) tb_dma(z, bi - 1, buf ^ 1u);
+        if (kTbBufs == 2 && bi) tb_dma(z, bi - 1, buf ^ 1u);
 #ifdef CCSX_TB_COUNTING
         const unsigned long long ts1 = stamp();
         z.pf[kPfTbSwitch] += ts1 - ts0;

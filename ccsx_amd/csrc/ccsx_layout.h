@@ -49,10 +49,12 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 //  * throughput: two waves (one helper), 4-row blocks, a 16-row ring of which
 //    the last 8 rows are read back -- up to 8 workgroups per CU, for slices of
 //    thousands of ZMWs, where resident ZMWs rather than per-ZMW latency bound
-//    the launch.
+//    the launch;
+//  * solo: one wave that also computes the decision bits, an 8-row ring and
+//    one traceback buffer -- up to 16 workgroups per CU (~10 KB of LDS each).
 // Each configuration's object reports its own LDS words and threads
 // (KCfgInfo), so the host never restates the build flags.
-enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1, kCfgThroughput = 2, kCfgCount = 3 };
+enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1, kCfgThroughput = 2, kCfgSolo = 3, kCfgCount = 4 };
 struct KCfgInfo {
     uint32_t lds_fixed_words;  // LDS words before the read buffer
     uint32_t threads;          // workgroup size

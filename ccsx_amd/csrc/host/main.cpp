@@ -54,6 +54,7 @@ struct Chunk {
     size_t id = 0;
     std::vector<Zmw> zs;
     std::atomic<size_t> pending{0};  // batches not yet back from a device
+    double t_read0 = 0, t_read1 = 0;  // CCSX_TIMING: when step 0's reader read it
 };
 
 struct Batch {
@@ -86,7 +87,7 @@ int usage()
             "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
             "CCSX_CHUNK     Largest chunk in ZMWs [16384 x min(groups, 4)]\n"
-            "CCSX_KCFG      Force a kernel configuration (0 latency, 1 occupancy, 2 throughput)\n"
+            "CCSX_KCFG      Force a kernel configuration (0 latency, 1 occupancy, 2 throughput, 3 solo)\n"
             "\n"
             "Arguments:\n"
             "input          Input file.\n"
@@ -185,6 +186,45 @@ private:
     std::condition_variable cv_;
     std::deque<Batch> q_;
     bool closed_ = false;
+};
+
+// chunks of ZMW references from step 0's reader to the preparing thread,
+// bounded (reading chunk k + 1 overlaps preparing chunk k); an empty chunk
+// ends the input
+class ReadQueue {
+public:
+    explicit ReadQueue(size_t limit) : limit_(limit) {}
+    void push(std::shared_ptr<Chunk> c)
+    {
+        std::unique_lock<std::mutex> g(m_);
+        space_.wait(g, [this] { return q_.size() < limit_ || stop_; });
+        q_.push_back(std::move(c));
+        ready_.notify_all();
+    }
+    std::shared_ptr<Chunk> pop()
+    {
+        std::unique_lock<std::mutex> g(m_);
+        ready_.wait(g, [this] { return !q_.empty(); });
+        auto c = std::move(q_.front());
+        q_.pop_front();
+        space_.notify_all();
+        return c;
+    }
+    void stop()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        space_.notify_all();
+    }
+
+private:
+    std::mutex m_;
+    std::condition_variable space_, ready_;
+    std::deque<std::shared_ptr<Chunk>> q_;
+    size_t limit_;
+    bool stop_ = false;
 };
 
 // chunks in input order, handed from step 0 to the writer; bounded so step 0
@@ -464,31 +504,45 @@ int main(int argc, char **argv)
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
     size_t chunk_max = 16384u * (size_t)std::min(ngroup, 4);
     if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));
-    size_t chunk_size = 1024;
-    for (size_t id = 0; !fatal; ++id) {
-        auto ch = std::make_shared<Chunk>();
-        ch->id = id;
-        std::vector<Zmw> &zs = ch->zs;
-        const double t0 = now_ms();
-        ccsx_ingest::ZmwRef zr;
-        int l;
-        while ((l = rd->next(zr)) >= 0) {
-            if (l < min_fulllen_count + 2) continue;
-            const uint64_t total = zr.total();
-            if (total > (uint64_t)max_subread_len || total < (uint64_t)min_subread_len) continue;
-            if (have_holes && hole_set.count(zr.hole)) continue;
-            zs.emplace_back();
-            zs.back().ref = std::move(zr);
-            if (zs.size() >= chunk_size) {
-                chunk_size = std::min(chunk_size * 4, chunk_max);
-                break;
+    // step 0's reading on its own thread, one chunk ahead of the preparation
+    // (the reference's step 0 does both in turn: main.c:652-697)
+    ReadQueue rq(1);
+    std::thread reader([&]() {
+        size_t chunk_size = 1024;
+        for (size_t id = 0;; ++id) {
+            auto ch = std::make_shared<Chunk>();
+            ch->id = id;
+            std::vector<Zmw> &zs = ch->zs;
+            ch->t_read0 = now_ms();
+            ccsx_ingest::ZmwRef zr;
+            int l;
+            while (!fatal && (l = rd->next(zr)) >= 0) {
+                if (l < min_fulllen_count + 2) continue;
+                const uint64_t total = zr.total();
+                if (total > (uint64_t)max_subread_len || total < (uint64_t)min_subread_len) continue;
+                if (have_holes && hole_set.count(zr.hole)) continue;
+                zs.emplace_back();
+                zs.back().ref = std::move(zr);
+                if (zs.size() >= chunk_size) {
+                    chunk_size = std::min(chunk_size * 4, chunk_max);
+                    break;
+                }
             }
+            ch->t_read1 = now_ms();
+            // kt_pipeline stops on an empty chunk (main.c:694-697); a chunk
+            // cut short by -1 (end of input or an invalid name) is processed
+            // and the next read goes on, as the reference's next step 0 does
+            const bool last = zs.empty();
+            rq.push(std::move(ch));
+            if (last) break;
         }
-        // kt_pipeline stops on an empty chunk (main.c:694-697); a chunk cut
-        // short by -1 (end of input or an invalid name) is processed and the
-        // next read goes on, as the reference's next step 0 does
-        if (zs.empty()) break;
-        const double t1 = now_ms();
+    });
+    for (;;) {
+        auto ch = rq.pop();
+        if (ch->zs.empty() || fatal) break;
+        std::vector<Zmw> &zs = ch->zs;
+        const size_t id = ch->id;
+        const double t0 = ch->t_read0, t1 = ch->t_read1;
         prepare_chunk(zs, nthreads, verbose);
         // cost-balanced micro-batches, longest first (dispatch.cpp)
         const uint32_t n = (uint32_t)zs.size();
@@ -509,6 +563,11 @@ int main(int argc, char **argv)
         ring.add(ch);  // blocks while 3 chunks are ahead of the writer
         queue.push(std::move(bs));
     }
+    // at the end of the input the reader has pushed its empty chunk and
+    // returned; after a fatal device error it stops at its next record and
+    // pushes without waiting for space
+    rq.stop();
+    reader.join();
     ring.finish();
     queue.close();
     for (auto &t : workers) t.join();

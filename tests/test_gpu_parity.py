@@ -246,14 +246,14 @@ def test_more_segments_than_lds_cursors(engine):
     _check(engine, [raw(segs), synth(7400, 2000, 6)], cx.MODE_SHRED)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
 def test_both_kernel_configs(engine, cfg, mode):
     """The latency (8-row DP blocks, 32-row ring), occupancy (4-row blocks,
-    24-row ring) and throughput (two-wave workgroups, 16-row ring) kernel
-    objects, each forced, on a mixed batch: short reads, a wide graph,
-    ordinary ZMWs (the by-size choice picks only one of them for small test
-    batches)."""
+    24-row ring), throughput (two-wave workgroups, 16-row ring) and solo
+    (one-wave workgroups, 8-row ring, one traceback buffer) kernel objects,
+    each forced, on a mixed batch: short reads, a wide graph, ordinary ZMWs
+    (the by-size choice picks only one of them for small test batches)."""
     zs = [synth(7400 + h, L, p) for h, (L, p) in enumerate([(2000, 8), (100, 12), (1500, 70), (4000, 6), (7000, 5)])]
     engine.set_kernel_cfg(cfg)
     try:
@@ -273,17 +273,19 @@ def test_shred_window_beyond_read_cap(engine):
     assert engine.rerun_count() - before >= 2
 
 
+@pytest.mark.parametrize("cfg", [2, 3])
 @pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
-def test_throughput_config_parity(engine, mode):
-    """The throughput configuration (one helper wave, ring read back 8 rows:
-    more rows take the far / spill path) forced on the parity shapes: config
+def test_throughput_config_parity(engine, mode, cfg):
+    """The throughput (one helper wave) and solo (no helper: the wave computes
+    its own decision bits) configurations, whose rings read back 8 rows (more
+    rows take the far / spill path), forced on the parity shapes: config
     B/C/D-like ZMWs, wide graphs, short reads and the edge cases."""
     cases = edge_cases()
     zs = [synth(7600 + h, L, p) for h, (L, p) in enumerate([(10000, 8), (2000, 30), (20000, 5), (1500, 70), (60, 12)])]
     zs += [cases[k] for k in cases]
-    engine.set_kernel_cfg(2)
+    engine.set_kernel_cfg(cfg)
     try:
         _check(engine, zs, mode)
-        assert engine.kernel_cfg() == 2
+        assert engine.kernel_cfg() == cfg
     finally:
         engine.set_kernel_cfg(-1)

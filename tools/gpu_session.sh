@@ -9,6 +9,7 @@
 #   parity             tests/test_gpu_parity.py only
 #   bench              the default bench.py line (config B, 20 steps, e2e, cpu baseline)
 #   bench:CFG[:KCFG]   bench.py --config CFG (B|C|D|E|H), 3 steps, optional forced kernel cfg
+#   benchn:CFG:N[:KCFG] the same with N ZMWs per GPU
 #   ab:CFG:KCFG,...[:LIB,...]  3 interleaved rounds of bench --config CFG over kernel cfgs x libraries
 #   e2e:N[:KCFG]       bench.py's end-to-end line (config E, ccsx_gpu_run) on N ZMWs per GPU
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
@@ -50,6 +51,10 @@ step() {
       fi
       local f="$OUT/bench_${cfg}${k:+_k$k}${CCSX_LIB:+_${CCSX_LIB%.so}}${CCSX_WG_PER_CU:+_w$CCSX_WG_PER_CU}.json"
       timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$k") > "$f" 2> "${f%.json}.err" &&
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['value'], 'ZMWs/s', d['gcups'], 'GCUPS', 'cfg', d['roofline'].get('kernel_cfg'))" "$f" ;;
+    benchn)  # benchn:CFG:N[:KCFG] -- bench.py --config CFG with N ZMWs per GPU
+      local f="$OUT/bench_${cfg}_n${k}${x:+_k$x}.json"
+      timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$x") --nzmw "$k" > "$f" 2> "${f%.json}.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], 'ms', d['value'], 'ZMWs/s', d['gcups'], 'GCUPS', 'cfg', d['roofline'].get('kernel_cfg'))" "$f" ;;
     ab)  # ab:CFG:KCFG[,KCFG...][:LIB,LIB...] -- 3 interleaved rounds over kernel cfgs x libraries
       local i kk f L libs
