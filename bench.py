@@ -191,8 +191,10 @@ def e2e_line(eng, rank: int, n: int, dist):
     t0 = time.perf_counter()
     res = eng.run_batch(batch, MODE_SHRED)
     t1 = time.perf_counter()
+    reruns0 = eng.rerun_count()
     res = eng.run_batch(batch, MODE_SHRED)
     t2 = time.perf_counter()
+    reruns = eng.rerun_count() - reruns0
     bad = sum(1 for r in res if r[0] != 0)
     if bad:
         raise SystemExit(f"e2e: device status != 0 for {bad} ZMWs")
@@ -207,7 +209,7 @@ def e2e_line(eng, rank: int, n: int, dist):
     return {"metric": "CCS ZMWs/sec end to end (host buffers in, CCS in host memory out)",
             "value": round(n * world / steady, 3), "unit": "ZMWs/s", "zmws_per_gpu": n, "s": round(steady, 3),
             "first_call_s": round(first, 3), "gbases_per_s": round(batch.bases * world / steady / 1e9, 3),
-            "gcups": round(cells * world / steady / 1e9, 3),
+            "gcups": round(cells * world / steady / 1e9, 3), "reruns": reruns,
             "workload": "config E slice: insert ~U[5,25] kb x passes ~U[5,12], 10% error, shredded mode, "
                         "prepared push lists in host memory (ingest timed separately: tools/ingest_bench)"}
 

@@ -185,6 +185,13 @@ struct ccsx_ctx {
     Slot slot[2];
     int32_t cfg_force = -1;            // test hook: -1 = by slice size
     uint32_t wg_cap = 0;               // measurement hook (CCSX_WG_PER_CU): LDS request padded to cap workgroups per CU
+    // LDS read buffer of tight-cap shredded slices, bases (CCSX_SHRED_READ_CAP):
+    // pushed windows are 2-3 kb unless a breakpoint is missed (+2 kb each,
+    // main.c:552-570); a longer one fails the ZMW with kErrReadLen and
+    // ccsx_gpu_run re-runs it uncapped.  4,096 rather than 8,192 bases: 2 KB
+    // less LDS per workgroup, 12 -> 14 solo workgroups per CU on config E
+    // (16,384-ZMW e2e 14.7k -> 17.1k ZMWs/s, no re-runs; r03o)
+    uint32_t shred_read_cap = 4096;
     uint32_t ncu = 256;                // compute units of the device
     uint64_t reruns = 0;               // ZMWs ccsx_gpu_run re-ran with full caps
     bool profiling = false;
@@ -250,6 +257,10 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
         const int v = atoi(k);
         if (v > 0 && v <= 16) c->wg_cap = (uint32_t)v;
     }
+    if (const char *k = getenv("CCSX_SHRED_READ_CAP")) {
+        const int v = atoi(k);
+        if (v >= 1024 && v <= 65536) c->shred_read_cap = (uint32_t)v;
+    }
     if (e != hipSuccess) {
         fprintf(stderr, "[ccsx_gpu] cannot open device %d: %s\n", device, hipGetErrorString(e));
         for (Slot &s : c->slot) s.release();
@@ -302,8 +313,6 @@ constexpr size_t kPinnedSeqFloor = 512ull << 20, kPinnedOutFloor = 128ull << 20;
 // (50 KiB of nibble pairs, 2 workgroups per CU) and 4,096 segments; beyond
 // them a slice runs the HBM-read instance
 constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
-// LDS read buffer of a tight-cap shredded slice (bases)
-constexpr uint32_t kShredReadCap = 8192;
 // slices of at least this many times the occupancy configuration's resident
 // workgroups run the solo configuration
 constexpr size_t kSoloSliceFactor = 3;
@@ -312,7 +321,7 @@ constexpr size_t kSoloSliceFactor = 3;
 // workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never
 // mix classes, so one long read does not shrink the occupancy of a slice
 // (shred_tight: a tight-cap shredded slice, whose LDS read buffer holds
-// kShredReadCap bases whatever the segment lengths -- pushed windows are
+// shred_read_cap bases whatever the segment lengths -- pushed windows are
 // 2-10 kb -- so only the cursor count sends it to the HBM-read instance)
 static int zmw_class(const ccsx_zmw_in &zi, bool shred_tight)
 {
@@ -406,12 +415,12 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
         s.lds_nmax = 0;
     } else {
         // shredded mode pushes windows of ~2-5 kb, not whole segments: with
-        // tight caps the buffer is capped at kShredReadCap bases (a longer
+        // tight caps the buffer is capped at shred_read_cap bases (a longer
         // window fails the ZMW with kErrReadLen and ccsx_gpu_run re-runs it
         // uncapped), which keeps the LDS of config-E slices small enough for
         // one more workgroup per CU
         uint32_t lb = std::max<uint32_t>(lmax_all, ccsx::kW);
-        if (shred_tight) lb = std::min(lb, kShredReadCap);
+        if (shred_tight) lb = std::min(lb, c->shred_read_cap);
         s.lds_read_words = (lb + 7) / 8 + 2;
         s.lds_nmax = std::max<uint32_t>(nmax, 1);
     }

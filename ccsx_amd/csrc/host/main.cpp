@@ -499,8 +499,11 @@ int main(int argc, char **argv)
     // step 0 (main.c:652-697) + the CPU half of step 1; the reference grows
     // the chunk 1,024 -> 4,096 -> 16,384 ZMWs (main.c:686-690), here the
     // last size scales with the devices (output order does not depend on it)
-    // micro-batches per context and chunk (CCSX_CTX_BATCHES, default 2)
-    uint32_t batches_per_ctx = 2;
+    // micro-batches per context and chunk (CCSX_CTX_BATCHES, default 1: a
+    // context's batch of a 16,384-ZMW chunk is then large enough for the
+    // solo kernel configuration; 100k config-E ZMWs from the generator's
+    // pipe 15.2 s with 2, 11.8 s with 1, r03o)
+    uint32_t batches_per_ctx = 1;
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
     size_t chunk_max = 16384u * (size_t)std::min(ngroup, 4);
     if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));

@@ -264,7 +264,7 @@ def test_both_kernel_configs(engine, cfg, mode):
 
 
 def test_shred_window_beyond_read_cap(engine):
-    """Shredded ZMWs whose pushed windows exceed the 8,192-base read buffer of
+    """Shredded ZMWs whose pushed windows exceed the 4,096-base read buffer of
     a tight-cap slice (with two passes the whole 12 kb and 9 kb segments are
     pushed, main.c:555-567): kErrReadLen, re-run uncapped, oracle parity."""
     zs = [synth(7500, 12000, 2), synth(7501, 2000, 8), synth(7502, 9000, 2)]

@@ -70,7 +70,7 @@ step() {
         done
       done ;;
     e2e)  # e2e:N[:KCFG] -- bench.py's config-E end-to-end line on N ZMWs (CCSX_KCFG forces a kernel cfg)
-      local f="$OUT/e2e_${cfg}${k:+_k$k}.json"
+      local f="$OUT/e2e_${cfg}${k:+_k$k}${CCSX_SHRED_READ_CAP:+_rc$CCSX_SHRED_READ_CAP}.json"
       CCSX_KCFG=${k:--1} CCSX_TIMING=1 timeout -k 10 600 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline \
         --e2e-zmws "$cfg" > "$f" 2> "${f%.json}.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1]))['e2e']; print(sys.argv[1], d['value'], 'ZMWs/s', d['s'], 's', d['gcups'], 'GCUPS', 'first', d['first_call_s'])" "$f" ;;
@@ -86,7 +86,7 @@ step() {
         > "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" 2> "$OUT/phase.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['kernel_ms'],2), 'ms', d['share'], d.get('two_wave'))" "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" ;;
     cli)  # cli:N[:pipe] -- tools/cli_stream.py: the CLI on N config-E ZMWs on stdin + oracle sample check
-      local tag="cli_$cfg${k:+_$k}${CCSX_SLOTS:+_s$CCSX_SLOTS}${CCSX_CHUNK:+_c$CCSX_CHUNK}"
+      local tag="cli_$cfg${k:+_$k}${CCSX_SLOTS:+_s$CCSX_SLOTS}${CCSX_CHUNK:+_c$CCSX_CHUNK}${CCSX_CTX_BATCHES:+_b$CCSX_CTX_BATCHES}${CCSX_KCFG:+_k$CCSX_KCFG}"
       timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" ${k:+--pipe} --out "$OUT/$tag" > "$OUT/$tag.log" 2>&1
       local rc=$?; tail -5 "$OUT/$tag.log"; return $rc ;;
     env)  # env:NAME=VALUE -- export for the following steps (env:NAME= unsets)
