@@ -344,13 +344,13 @@ static void zmw_extent(const ccsx_zmw_in &zi, uint64_t &S, uint64_t &hi, uint32_
 }
 
 // device bytes one ZMW occupies when staged
-static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, uint32_t tight_rows, bool shred)
+static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, uint32_t tight_rows, uint32_t shred_win)
 {
     uint64_t S, hi;
     uint32_t lmax;
     zmw_extent(zi, S, hi, lmax);
     ccsx::ZmwDesc d{};
-    ccsx::zcaps(d, S, lmax, zi.nseg, full, tight_rows, shred);
+    ccsx::zcaps(d, S, lmax, zi.nseg, full, tight_rows, shred_win);
     ccsx::ZLayout L;
     ccsx::zlayout(L, d);
     return ccsx::align256(L.total) + hi + d.outcap + uint64_t(zi.nseg) * 8 + sizeof(ccsx::ZmwDesc) + 32;
@@ -379,7 +379,7 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
             return -1;
         }
         ccsx::ZmwDesc &d = s.desc[i];
-        ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows, c->shred_caps);
+        ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
         d.seg0 = nseg;
         d.seq_off = seq_b;
         seq_b += hi;
@@ -776,7 +776,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             uint64_t need = 0;
             size_t e = b;
             while (e < idx.size()) {
-                const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows, c->shred_caps);
+                const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
                 if (e > b && (need + x > slot_budget || cls[idx[e]] != cls[idx[b]])) break;
                 need += x;
                 ++e;

@@ -47,6 +47,13 @@ namespace CCSX_KCFG {
 #ifndef CCSX_BLK
 #define CCSX_BLK 8
 #endif
+// helper waves per workgroup: 2 (latency / occupancy configurations), 1
+// (throughput configuration: two-wave workgroups, twice the resident ZMWs) or
+// 0 (solo configuration: one wave computes the decision bits too, dp_solo)
+#ifndef CCSX_HELPERS
+#define CCSX_HELPERS 2
+#endif
+constexpr int kHelpers = CCSX_HELPERS;
 
 constexpr int kO = -3, kE = -2, kMs = 2, kXs = -6;  // main.c:842-847
 enum { HC_MPRED = 0, HC_MSRC = 1, HC_DEL = 2, HC_INS = 3 };
@@ -327,10 +334,12 @@ __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
 }
 
 // LDS layout of a workgroup (int32 words)
+// (the solo object has no helpers: no diagnostic slots or band-offset ring,
+// which keeps a config-D workgroup within 10 KB, 16 per CU)
 constexpr int kLdsRing = 0;                              // kRingA DP rows x kRowW (traceback: 2 blocks)
 constexpr int kLdsDiag = kLdsRing + kRingA * kRowW;      // 32: helpers' diagnostic counters at exit
-constexpr int kLdsOffRing = kLdsDiag + 32;               // 64: band offset of DP row q at q & 63
-constexpr int kLdsJob = kLdsOffRing + 64;                // 16: DP job / results
+constexpr int kLdsOffRing = kLdsDiag + (kHelpers ? 32 : 0);  // 64: band offset of DP row q at q & 63
+constexpr int kLdsJob = kLdsOffRing + (kHelpers ? 64 : 0);   // 16: DP job / results
 constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
 
@@ -393,13 +402,6 @@ __device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; 
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
 constexpr int kBlkAB = CCSX_BLK;  // rows per lockstep block: helper h takes rows r0 + h, r0 + h + 2, ...
-// helper waves per workgroup: 2 (latency / occupancy configurations), 1
-// (throughput configuration: two-wave workgroups, twice the resident ZMWs) or
-// 0 (solo configuration: one wave computes the decision bits too, dp_solo)
-#ifndef CCSX_HELPERS
-#define CCSX_HELPERS 2
-#endif
-constexpr int kHelpers = CCSX_HELPERS;
 static_assert(kHelpers >= 0 && kHelpers <= 2, "zero, one or two helper waves");
 constexpr int kBlockThreads = 64 * (1 + kHelpers);
 constexpr int kHelperStep = kHelpers ? kHelpers : 1;
@@ -1446,10 +1448,10 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
 }
 
-template <bool LM>
+template <int LM>
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid);
 __device__ __forceinline__ void columns_count(const Z &z, uint32_t n, uint32_t ncols, uint32_t tid, uint32_t T);
-__device__ __forceinline__ bool merge_in_lds(uint32_t R);
+__device__ __forceinline__ int merge_in_lds(uint32_t R);
 
 // helper wave h (1 + h = wave index): serve DP and merge jobs until wave 0
 // posts kJobExit
@@ -1474,8 +1476,10 @@ __device__ __forceinline__ void dp_helper(Z &z, uint32_t h)
             // merge's row-parallel phases are on the critical path: raise the
             // helpers above other workgroups' DP helpers (below any wave 0)
             __builtin_amdgcn_s_setprio(kPrioMerge);
-            if (merge_in_lds(z.R)) merge<true>(z, uni(job->k), m, threadIdx.x);
-            else merge<false>(z, uni(job->k), m, threadIdx.x);
+            const int lm = merge_in_lds(z.R);
+            if (lm == 2) merge<2>(z, uni(job->k), m, threadIdx.x);
+            else if (lm == 1) merge<1>(z, uni(job->k), m, threadIdx.x);
+            else merge<0>(z, uni(job->k), m, threadIdx.x);
             __builtin_amdgcn_s_setprio(0);
         }
         else if (m >= (uint32_t)kW) dp_wave_b<true>(z, m, h);
@@ -2044,17 +2048,23 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
 // workgroup barriers (which also make the HBM writes visible); M1's ordered
 // compaction and the two prefix scans run on wave 0 between barriers.  Every
 // branch that skips a barrier is uniform over the workgroup.
-// LM: the graph is small enough (every shredding window) for the current
-// rows' node bytes and the new-row counts / shifts to live in the DP ring's
-// LDS (idle during merge): the column walks, the count atomics, the prefix
-// scan and every shift lookup are then LDS accesses instead of dependent HBM
-// round trips.  Larger graphs (-P) take the same steps through HBM.
-__device__ __forceinline__ bool merge_in_lds(uint32_t R)
+// LM = 2: the graph is small enough (every shredding window of the three-
+// wave objects) for the current rows' node bytes and the new-row counts /
+// shifts to live in the DP ring's LDS (idle during merge): the column walks,
+// the count atomics, the prefix scan and every shift lookup are then LDS
+// accesses instead of dependent HBM round trips.  LM = 1 (the solo object's
+// 8.7 KB ring, graphs of 1,728-8,700 rows): the node bytes alone, the counts
+// in HBM.  LM = 0: larger graphs (-P) take the same steps through HBM.
+__device__ __forceinline__ int merge_in_lds(uint32_t R)
 {
-    return (R + 1) * 5u + 64u <= (uint32_t)(kRingA * kRowW * 4);
+    constexpr uint32_t bytes = (uint32_t)(kRingA * kRowW * 4);
+#ifndef CCSX_MERGE_LM1
+#define CCSX_MERGE_LM1 1
+#endif
+    return (R + 1) * 5u + 64u <= bytes ? 2 : (CCSX_MERGE_LM1 && R + 64u <= bytes) ? 1 : 0;
 }
 
-template <bool LM>
+template <int LM>
 __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid)
 {
     constexpr uint32_t T = kBlockThreads;
@@ -2064,10 +2074,12 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     const uint32_t R = z.R, nw = z.d.nw;
     const int a = z.cur, b = a ^ 1;
     const uint8_t *nbg = G_nb(z, a);
-    uint32_t *lcnt = reinterpret_cast<uint32_t *>(z.lds + kLdsRing);  // LM: counts / shifts, R + 1 words
-    uint8_t *lnb = reinterpret_cast<uint8_t *>(lcnt + R + 1);          // LM: node bytes, R (+ 3) bytes
+    uint32_t *lcnt = reinterpret_cast<uint32_t *>(z.lds + kLdsRing);  // LM 2: counts / shifts, R + 1 words
+    // node bytes, R (+ 3) bytes: after the counts (LM 2) or alone (LM 1)
+    uint8_t *lnb = reinterpret_cast<uint8_t *>(LM == 2 ? lcnt + R + 1 : lcnt);
     if (LM) {
-        for (uint32_t x = tid; x <= R; x += T) lcnt[x] = 0;
+        if (LM == 2)
+            for (uint32_t x = tid; x <= R; x += T) lcnt[x] = 0;
         for (uint32_t x = 4 * tid; x < R; x += 4 * T)
             *reinterpret_cast<uint32_t *>(lnb + x) = *reinterpret_cast<const uint32_t *>(nbg + x);
         __syncthreads();
@@ -2085,7 +2097,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     uint32_t *ipt = P<uint32_t>(z, z.L.ipt);
     uint8_t *iinf = P<uint8_t>(z, z.L.iinf);
     uint32_t *ifix = P<uint32_t>(z, z.L.ifix);
-    uint32_t *cnt = LM ? lcnt : P<uint32_t>(z, z.L.cnt);
+    uint32_t *cnt = LM == 2 ? lcnt : P<uint32_t>(z, z.L.cnt);
     uint8_t *fixf = P<uint8_t>(z, z.L.fixf);
     uint32_t *addp = P<uint32_t>(z, z.L.addp);
     uint32_t *cntn = P<uint32_t>(z, z.L.cntn);
@@ -2156,7 +2168,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     DP_STAMP(kPfRowA);
     // M2: shift[x] = #new items with point <= x
     for (uint32_t x = tid; x <= R; x += T) {
-        if (!LM) cnt[x] = 0;
+        if (LM != 2) cnt[x] = 0;
         fixf[x] = 0;
     }
     __syncthreads();
@@ -2491,8 +2503,10 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             volatile DpJob *job = dp_job(z);
             if (lane_id() == 0) job->kind = kJobMerge, job->m = m, job->R = z.R, job->cur = (uint32_t)z.cur, job->k = k;
             __syncthreads();  // J: job posted
-            if (merge_in_lds(z.R)) merge<true>(z, k, m, threadIdx.x);
-            else merge<false>(z, k, m, threadIdx.x);
+            const int lm = merge_in_lds(z.R);
+            if (lm == 2) merge<2>(z, k, m, threadIdx.x);
+            else if (lm == 1) merge<1>(z, k, m, threadIdx.x);
+            else merge<0>(z, k, m, threadIdx.x);
         }
         if (z.status) return 0;
         staged = k + 1 < z.d.n;  // (the merge staged read k + 1 under run_poa's own checks)

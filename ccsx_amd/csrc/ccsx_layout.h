@@ -184,19 +184,22 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 // a fraction of the memory; every cap is checked on the device (kErrRows,
 // kErrEdges, kErrSpill) and ccsx_gpu_run re-runs a ZMW that hits
 // one with full caps.  tight_rows overrides the tight row cap (tests).
-// shred: the ZMW runs the shredded loop (main.c:541-641), whose POAs are of
-// 2 kb windows (+2 kb per missed breakpoint) rather than whole segments, so
-// the tight row cap follows the window, not the segment (rows ~ window x
-// (1 + ~0.07 reads): 3 x 8,000 + 4,096 covers windows up to ~8 kb).
+// shred_win: the ZMW runs the shredded loop (main.c:541-641) with pushed
+// windows of at most shred_win bases (the LDS read buffer of a tight-cap
+// slice; a longer window fails the ZMW and it is re-run uncapped), whose POAs
+// are of 2 kb windows (+2 kb per missed breakpoint) rather than whole
+// segments, so the tight row cap follows the window, not the segment (rows ~
+// window x (1 + ~0.07 reads): 3 x 4,096 + 4,096 covers 4 kb windows of up to
+// ~40 reads).  0: not shredded.
 CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, bool full = true,
-                          uint32_t tight_rows = 0, bool shred = false)
+                          uint32_t tight_rows = 0, uint32_t shred_win = 0)
 {
     d.n = n;
     d.rcap = uint32_t(S + 16);
     d.ecap = uint32_t(S + n + 16);
     d.scap = d.rcap / 4 + 64;
     if (!full) {
-        const uint64_t lw = shred && lmax > 8000u ? 8000u : lmax;
+        const uint64_t lw = shred_win && lmax > shred_win ? shred_win : lmax;
         uint64_t r = tight_rows ? tight_rows : 3ull * lw + 4096;
         if (r < S) {
             d.rcap = uint32_t(r + 16);

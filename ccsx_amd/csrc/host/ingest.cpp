@@ -741,12 +741,19 @@ std::unique_ptr<ZmwSource> ZmwSource::open(const char *path, bool is_bam, int nt
     const char *e = getenv("CCSX_INGEST_BLOCK");
     const size_t block = e ? (size_t)std::max<long>(1, atol(e)) : (32u << 20);
     std::unique_ptr<ByteSource> src;
+    // stdin redirected from a regular file, not read yet: the file's own
+    // path below (mmap, parallel BGZF, gzread), else a gzread stream
+    bool stdin_stream = false;
     if (strcmp(path, "-") == 0) {
+        struct stat st;
+        stdin_stream = !(fstat(0, &st) == 0 && S_ISREG(st.st_mode) && lseek(0, 0, SEEK_CUR) == 0);
+    }
+    if (stdin_stream) {
         gzFile g = gzdopen(dup(0), "rb");
         if (!g) return nullptr;
         src.reset(new GzSource(g));
     } else {
-        const int fd = ::open(path, O_RDONLY);
+        const int fd = strcmp(path, "-") == 0 ? dup(0) : ::open(path, O_RDONLY);
         if (fd < 0) return nullptr;
         unsigned char h[18];
         const ssize_t k = pread(fd, h, sizeof h, 0);

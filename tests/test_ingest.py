@@ -78,3 +78,31 @@ def test_ingest_bench_reports_throughput(tmp_path, ingest_bench):
     r = json.loads(subprocess.run([ingest_bench, fa, "0", "2", "16"], check=True, capture_output=True,
                                   text=True).stdout)
     assert r["zmws"] == 40 and r["bases"] > 40 * 6 * 3000
+
+
+@pytest.mark.parametrize("fmt", ["fa", "fa.gz", "bgzf.fa.gz", "bam"])
+@pytest.mark.parametrize("how", ["redirect", "pipe"])
+def test_stdin_matches_reader(tmp_path, ingest_bench, fmt, how):
+    """INPUT "-" (main.c:804-808): stdin redirected from a regular file takes
+    the file's own path (mmap / parallel BGZF / gzread), a pipe the gzread
+    stream; both give what the reader gives for the named file."""
+    fa = str(tmp_path / "in.fa")
+    write(fa, 40, 1200, 6)
+    path, is_bam = fa, 0
+    if fmt == "fa.gz":
+        path = fa + ".gz"
+        with open(fa, "rb") as s, gzip.open(path, "wb") as d:
+            d.write(s.read())
+    elif fmt == "bgzf.fa.gz":
+        path = str(tmp_path / "in.bgzf.fa.gz")
+        _bgzip(fa, path)
+    elif fmt == "bam":
+        path, is_bam = str(tmp_path / "in.bam"), 1
+        write_bam(path, records(40, 1200, 6))
+    cmd = [ingest_bench, "-", str(is_bam), "3", "16", "--dump"]
+    if how == "redirect":
+        with open(path, "rb") as f:
+            got = subprocess.run(cmd, stdin=f, check=True, capture_output=True).stdout
+    else:
+        got = subprocess.run(cmd, input=open(path, "rb").read(), check=True, capture_output=True).stdout
+    assert got.decode().splitlines() == _expected(path, bool(is_bam))

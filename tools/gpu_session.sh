@@ -14,6 +14,7 @@
 #   e2e:N[:KCFG]       bench.py's end-to-end line (config E, ccsx_gpu_run) on N ZMWs per GPU
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
+#   prof:CFG           tools/profile_gpu.sh: kernel trace of bench's timed run + PMC passes (traffic) of CFG
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
 #   cli:N[:pipe]       CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py)
 #   env:NAME=VALUE     export NAME for the following steps (env:NAME= unsets it)
@@ -80,6 +81,8 @@ step() {
         echo "kt $cfg done" ;;
     pmc)
       timeout -k 10 900 bash "$R/tools/pmc_pass.sh" "$TAG/pmc_$cfg" --config "$cfg" > "$OUT/pmc_$cfg.log" 2>&1 && echo "pmc $cfg done" ;;
+    prof)
+      CFG=$cfg timeout -k 10 1000 bash "$R/tools/profile_gpu.sh" "${TAG}_$cfg" > "$OUT/prof_$cfg.log" 2>&1 && echo "prof $cfg done" ;;
     phase)  # phase:L,PASSES,N:KCFG  (per-ZMW cycle split; CCSX_LIB=libccsx_amd_diag.so for the DP detail)
       local L P N; IFS=, read -r L P N <<< "$cfg"
       timeout -k 10 600 python -u tools/phase_prof.py --L "$L" --passes "$P" --n "$N" --kcfg "${k:--1}" \

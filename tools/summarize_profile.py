@@ -78,7 +78,7 @@ for f in ("kt_kernel_stats.csv",):
     p = glob.glob(os.path.join(src, "kt", "*" + f))
     if p:
         open(os.path.join(ROOT, "profiles", f"{tag}_{f}"), "w").write(open(p[0]).read())
-cfg = {"B": "B"}.get(sys.argv[2] if len(sys.argv) > 2 else "B", "B")
+cfg = sys.argv[2] if len(sys.argv) > 2 else "B"  # the bench config profiled (traffic.json key)
 tj = os.path.join(ROOT, "profiles", "traffic.json")
 t = json.load(open(tj)) if os.path.exists(tj) else {}
 t[cfg] = {"bytes_per_launch": fetch_b + write_b, "fetch_bytes": fetch_b, "write_bytes": write_b,
