@@ -2,14 +2,15 @@
 stdin (main.c:804-808: INPUT "-"), timed end to end, with a random sample of
 its output checked byte for byte against the oracle on the same ZMWs.
 
-    cli_stream.py --n 100000 [--hole0 H] [--jobs 16] [--sample 1000] [--pipe] --out DIR
+    cli_stream.py --n 100000 [--hole0 H] [--jobs 16] [--sample 1000] [--pipe | --fifo-out] --out DIR
 
 The input is tools/synth_fa's config-E FASTA (insert ~U[5,25] kb x 5-12
 passes, 10 % error), written to a file first and fed on stdin (--pipe: the
 generator's stdout piped straight into the CLI, so the generator's own rate
 bounds the run, and the CLI's output read from a FIFO by a thread that keeps
 only the sampled records: nothing touches the disk, so a 500k-ZMW run needs
-neither 65 GB of input nor 7.5 GB of output on the box).  Writes
+neither 65 GB of input nor 7.5 GB of output on the box; --fifo-out: the
+input from a file as usual, the output through the FIFO).  Writes
 DIR/cli_stream.json and DIR/cli_stream_timing.log.
 Test infrastructure: the oracle is only the checker of the sample."""
 import argparse
@@ -36,12 +37,13 @@ def main():
     ap.add_argument("--jobs", type=int, default=16)
     ap.add_argument("--sample", type=int, default=1000)
     ap.add_argument("--pipe", action="store_true")
+    ap.add_argument("--fifo-out", action="store_true")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="ccsx_stream_")
     fa, ccs = os.path.join(tmp, "in.fa"), os.path.join(tmp, "out.fa")
-    res = {"n": a.n, "hole0": a.hole0, "jobs": a.jobs, "pipe": a.pipe,
+    res = {"n": a.n, "hole0": a.hole0, "jobs": a.jobs, "pipe": a.pipe, "fifo_out": a.fifo_out or a.pipe,
            "workload": "config E: insert ~U[5,25] kb x passes ~U[5,12] (total <= 450 kb), 10% error, FASTA on stdin, "
                        "shredded mode"}
     gen = [GEN, str(a.n), str(a.hole0), "0", "0", str(a.jobs)]
@@ -95,17 +97,29 @@ def main():
             res["gen_s"] = time.perf_counter() - t0
             res["input_bytes"] = os.path.getsize(fa)
             print(f"input: {res['input_bytes'] / 1e9:.2f} GB in {res['gen_s']:.1f} s", flush=True)
+            rd = None
+            if a.fifo_out:
+                os.mkfifo(ccs)
+                rd = threading.Thread(target=read_output, args=(ccs,))
+                rd.start()
             t0 = time.perf_counter()
             with open(fa, "rb") as f:
                 r = subprocess.run([BIN, "-A", "-j", str(a.jobs), "-", ccs], stdin=f, stderr=log, env=env)
             res["cli_s"] = time.perf_counter() - t0
+            if rd is not None:
+                if r.returncode != 0:
+                    try:
+                        os.close(os.open(ccs, os.O_WRONLY | os.O_NONBLOCK))
+                    except OSError:
+                        pass
+                rd.join()
         log.close()
         if r.returncode != 0:
             raise SystemExit(f"ccsx exited {r.returncode}")
         res["zmws_per_s"] = a.n / res["cli_s"]
         print(f"cli: {a.n} ZMWs in {res['cli_s']:.2f} s = {res['zmws_per_s']:.0f} ZMWs/s", flush=True)
         # the output: one record per ZMW with a CCS, in input (hole) order
-        if not a.pipe:
+        if not (a.pipe or a.fifo_out):
             read_output(ccs)
         got = scan["got"]
         res["records"] = scan["nrec"]

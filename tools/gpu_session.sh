@@ -16,7 +16,8 @@
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
 #   prof:CFG           tools/profile_gpu.sh: kernel trace of bench's timed run + PMC passes (traffic) of CFG
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
-#   cli:N[:pipe]       CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py)
+#   cli:N[:pipe|:fifo] CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py;
+#                      pipe: generator piped in, fifo: output through a FIFO)
 #   env:NAME=VALUE     export NAME for the following steps (env:NAME= unsets it)
 #   lib:NAME           the following steps load ccsx_amd/NAME (CCSX_LIB); lib: resets
 # Environment: CCSX_LIB selects a library variant for the bench steps; CCSX_WG_PER_CU caps the
@@ -90,7 +91,8 @@ step() {
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['kernel_ms'],2), 'ms', d['share'], d.get('two_wave'))" "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" ;;
     cli)  # cli:N[:pipe] -- tools/cli_stream.py: the CLI on N config-E ZMWs on stdin + oracle sample check
       local tag="cli_$cfg${k:+_$k}${CCSX_SLOTS:+_s$CCSX_SLOTS}${CCSX_CHUNK:+_c$CCSX_CHUNK}${CCSX_CTX_BATCHES:+_b$CCSX_CTX_BATCHES}${CCSX_KCFG:+_k$CCSX_KCFG}"
-      timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" ${k:+--pipe} --out "$OUT/$tag" > "$OUT/$tag.log" 2>&1
+      local flag=""; [ "$k" = pipe ] && flag=--pipe; [ "$k" = fifo ] && flag=--fifo-out
+      timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" $flag --out "$OUT/$tag" > "$OUT/$tag.log" 2>&1
       local rc=$?; tail -5 "$OUT/$tag.log"; return $rc ;;
     env)  # env:NAME=VALUE -- export for the following steps (env:NAME= unsets)
       if [ -n "${cfg#*=}" ]; then export "$cfg"; else unset "${cfg%%=*}"; fi ;;
