@@ -2189,7 +2189,10 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     __syncthreads();
     // (MB read bases per thread per pass: their dependent loads are issued
     // together so the HBM round trips overlap)
-    constexpr uint32_t MB = 4;
+#ifndef CCSX_MERGE_MB
+#define CCSX_MERGE_MB 4
+#endif
+    constexpr uint32_t MB = CCSX_MERGE_MB;
     for (uint32_t j0 = 1 + tid; j0 < m; j0 += MB * T) {
         uint32_t sv[MB], dv[MB], e0[MB], e1[MB], p0[MB], p1[MB];
 #pragma unroll
@@ -2288,7 +2291,10 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     uint4 *rrec = P<uint4>(z, z.L.rrec);
     uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
     // (PB rows per thread per pass, loads first)
-    constexpr uint32_t PB = 2;
+#ifndef CCSX_MERGE_PB
+#define CCSX_MERGE_PB 2
+#endif
+    constexpr uint32_t PB = CCSX_MERGE_PB;
     for (uint32_t x0 = tid; x0 < R; x0 += PB * T) {
       uint32_t bn[PB], be0[PB], be1[PB], bad[PB], bo[PB], bq[PB][4];
 #pragma unroll
