@@ -39,8 +39,9 @@ KCFGS = [(n, [f"-DCCSX_KCFG={n}", f"-DCCSX_LAUNCH=ccsx_launch_zmw_{n}", f"-DCCSX
                       # no issue priorities: two wave 0s share each SIMD (A/B r03g: D 567 -> 550 ms)
                       ("tput", ["-DCCSX_RINGA=16", "-DCCSX_BLK=4", "-DCCSX_RING=8", "-DCCSX_HELPERS=1",
                                 "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0"]),
-                      # one-wave workgroups (dp_solo), an 8-row ring, one traceback buffer
-                      ("solo", ["-DCCSX_RINGA=8", "-DCCSX_BLK=4", "-DCCSX_RING=8", "-DCCSX_HELPERS=0",
+                      # one-wave workgroups (dp_solo), an 8-row ring, one traceback buffer;
+                      # 8-row blocks (no barriers: only the unrolling; A/B r03u: D 363.6 -> 356.8 ms)
+                      ("solo", ["-DCCSX_RINGA=8", "-DCCSX_BLK=8", "-DCCSX_RING=8", "-DCCSX_HELPERS=0",
                                 "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0"])]]
 
 

@@ -289,3 +289,26 @@ def test_throughput_config_parity(engine, mode, cfg):
         assert engine.kernel_cfg() == cfg
     finally:
         engine.set_kernel_cfg(-1)
+
+
+@pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
+def test_solo_config_hbm_read_instance(engine, mode):
+    """The solo object (one wave, dp_solo's own read-window slides, one
+    traceback buffer) forced on the HBM-read instance's shapes: 110 kb
+    segments (-P pushes them whole) and a ZMW of 4,200 segments (its cursors
+    live in the workspace), beside an ordinary ZMW."""
+    import random
+    rnd = random.Random(12)
+    ins = bytes(rnd.choice(b"ACGT") for _ in range(60))
+    segs = []
+    for _ in range(4200):
+        s = bytearray(ins)
+        s[rnd.randrange(60)] = rnd.choice(b"ACGT")
+        segs.append(bytes(s))
+    zs = [synth(7700, 110_000, 3), raw(segs), synth(7701, 3000, 6)]
+    engine.set_kernel_cfg(3)
+    try:
+        _check(engine, zs, mode)
+        assert engine.kernel_cfg() == 3
+    finally:
+        engine.set_kernel_cfg(-1)

@@ -3,7 +3,7 @@
 # timing (tools/gpu_ab.sh).  The flags go to every kernel configuration
 # (after its own defines, so they override them) and to the host launcher;
 # the configurations' defines come from ccsx_amd/build.py (KCFGS).
-#   [CFGS="tput occ"] [KSRC=path/to/kernel.hip] tools/build_variant.sh TAG -DFOO=1 ...
+#   [CFGS="tput occ"] [KSRC=path/to/kernel.hip] [KSCHED="..."] tools/build_variant.sh TAG -DFOO=1 ...
 # CFGS limits the extra flags to the named configurations (default: all).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -11,7 +11,8 @@ TAG=$1; shift
 OBJ=$ROOT/build/obj
 C=$ROOT/ccsx_amd/csrc
 INC="-I$ROOT/include -I$C -I$C/host"
-K="/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC -mllvm -amdgpu-sched-strategy=max-ilp -Wno-macro-redefined"
+# KSCHED overrides the machine-scheduler flags (default: build.py's max-ilp; KSCHED=" " for LLVM's default)
+K="/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC ${KSCHED:--mllvm -amdgpu-sched-strategy=max-ilp} -Wno-macro-redefined"
 KOBJS=""
 while read -r NAME DEFS; do
   X=("$@")
