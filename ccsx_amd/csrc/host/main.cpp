@@ -87,6 +87,7 @@ int usage()
             "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
             "CCSX_CHUNK     Largest chunk in ZMWs [16384 x min(groups, 4)]\n"
+            "CCSX_CHUNK0    First chunk in ZMWs [1024], growing x4 up to CCSX_CHUNK\n"
             "CCSX_KCFG      Force a kernel configuration (0 latency, 1 occupancy, 2 throughput, 3 solo)\n"
             "\n"
             "Arguments:\n"
@@ -515,8 +516,12 @@ int main(int argc, char **argv)
     // step 0's reading on its own thread, one chunk ahead of the preparation
     // (the reference's step 0 does both in turn: main.c:652-697)
     ReadQueue rq(1);
+    // first chunk: the reference's 1,024 (CCSX_CHUNK0 overrides; the chunk
+    // sizes change only how the work is cut, never the output)
+    size_t chunk0 = 1024;
+    if (const char *e = getenv("CCSX_CHUNK0")) chunk0 = std::max<size_t>(1, std::min<size_t>(chunk_max, strtoull(e, nullptr, 10)));
     std::thread reader([&]() {
-        size_t chunk_size = 1024;
+        size_t chunk_size = chunk0;
         for (size_t id = 0;; ++id) {
             auto ch = std::make_shared<Chunk>();
             ch->id = id;

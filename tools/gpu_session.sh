@@ -90,7 +90,7 @@ step() {
         > "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" 2> "$OUT/phase.err" &&
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['kernel_ms'],2), 'ms', d['share'], d.get('two_wave'))" "$OUT/phase_${L}_${P}_${N}_k${k}${CCSX_LIB:+_$CCSX_LIB}.json" ;;
     cli)  # cli:N[:pipe] -- tools/cli_stream.py: the CLI on N config-E ZMWs on stdin + oracle sample check
-      local tag="cli_$cfg${k:+_$k}${CCSX_SLOTS:+_s$CCSX_SLOTS}${CCSX_CHUNK:+_c$CCSX_CHUNK}${CCSX_CTX_BATCHES:+_b$CCSX_CTX_BATCHES}${CCSX_KCFG:+_k$CCSX_KCFG}"
+      local tag="cli_$cfg${k:+_$k}${CCSX_SLOTS:+_s$CCSX_SLOTS}${CCSX_CHUNK:+_c$CCSX_CHUNK}${CCSX_CHUNK0:+_f$CCSX_CHUNK0}${CCSX_CTX_BATCHES:+_b$CCSX_CTX_BATCHES}${CCSX_KCFG:+_k$CCSX_KCFG}"
       local flag=""; [ "$k" = pipe ] && flag=--pipe; [ "$k" = fifo ] && flag=--fifo-out
       timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" $flag --out "$OUT/$tag" > "$OUT/$tag.log" 2>&1
       local rc=$?; tail -5 "$OUT/$tag.log"; return $rc ;;
