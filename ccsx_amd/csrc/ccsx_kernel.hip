@@ -984,6 +984,55 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
     }
 }
 
+// Row r's decision bits from its cell values (SPEC.md §3.4: code, D-ext,
+// I-ext, M / D tags), its free-end candidates (§3.5) and the record store:
+// the helpers' dpB_tail (values recomputed from the ring) and the solo
+// dpS_row (values the wave holds) share it.  mp / d: M came from a
+// predecessor / D beat M, per cell; X = H' + 2 t; Pex = the insertion scan's
+// exclusive prefix max.  maybe_wide: the row may have more than 63
+// predecessors (its slots also go to the wide slot records).
+template <bool FULL>
+__device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, int32_t &bOff,
+                                           const __amdgpu_buffer_rsrc_t &rc, uint32_t r, uint32_t m, int32_t lim,
+                                           int32_t off, uint32_t np, bool maybe_wide, const PredAcc &A, const LaneK &c,
+                                           bool mp0, bool mp1, bool d0, bool d1, int32_t hp0, int32_t hp1, int32_t X0,
+                                           int32_t X1, int32_t Pex)
+{
+    const int lane = lane_id();
+    const int32_t X1L = wave_shr1(INT32_MAX, X1);
+    const int32_t ex1 = max(Pex, X0);
+    const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
+    const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
+    const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
+    const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
+    uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
+    uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
+    if (maybe_wide && __builtin_expect(np > 63u, 0)) {
+        // wide slot record of row r: u16 M / D slots per cell
+        reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
+            make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
+    }
+    // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
+    // H' at j = m - 1
+    const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
+    int32_t e0 = X0 + eb;
+    int32_t e1 = X1 + eb;
+    if (FULL) {
+        e1 += (off == lim && lane == 63) ? 3 : 0;
+    } else {
+        if ((uint32_t)c.L2 == m - 1) e0 += 3;
+        if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
+        if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
+        if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
+    }
+    // rows come in order: the first maximum is the earliest (min row, min cell)
+    if (e0 > bE) bE = e0, bKey = r * 2, bOff = off;
+    if (e1 > bE) bE = e1, bKey = r * 2 + 1, bOff = off;
+    // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
+    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
+                                          0);
+}
+
 // helper wave: everything after the predecessor terms of row r (SPEC.md
 // §3.2-§3.5): M, H', the insertion scan, the cell codes and tags, the
 // free-end candidates, the record store
@@ -1003,38 +1052,8 @@ __device__ __forceinline__ void dpB_tail(Z &z, BState &S, uint32_t r, uint32_t m
     // insertions (SPEC.md §3.4): the same prefix-max scan as wave 0's
     const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
     const int32_t Pex = wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
-    const int32_t X1L = wave_shr1(INT32_MAX, X1);
-    const int32_t ex1 = max(Pex, X0);
-    const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
-    const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
-    const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
-    const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
-    uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
-    uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
-    if (__builtin_expect(np > 63u, 0)) {
-        // wide slot record of row r: u16 M / D slots per cell
-        reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
-            make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
-    }
-    // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
-    // H' at j = m - 1
-    const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
-    int32_t e0 = X0 + eb;
-    int32_t e1 = X1 + eb;
-    if (FULL) {
-        e1 += (off == lim && lane == 63) ? 3 : 0;
-    } else {
-        if ((uint32_t)c.L2 == m - 1) e0 += 3;
-        if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
-        if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
-        if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
-    }
-    // rows come in order: the first maximum is the earliest (min row, min cell)
-    if (e0 > S.bE) S.bE = e0, S.bKey = r * 2, S.bOff = off;
-    if (e1 > S.bE) S.bE = e1, S.bKey = r * 2 + 1, S.bOff = off;
-    // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
-    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), S.rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
-                                          0);
+    row_record<FULL>(z, S.bE, S.bKey, S.bOff, S.rc, r, m, lim, off, np, true, A, c, mp0, mp1, d0, d1, hp0, hp1, X0, X1,
+                     Pex);
 }
 
 // helper wave: the decision bits of one row (wave 0 wrote its ring row and
@@ -1308,35 +1327,10 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
         S.pOff = off;
         S.pArg = off + 127 - (key & 127);
-        // decision bits (SPEC.md §3.4): code, D-ext, I-ext, M / D tags
-        const int32_t X1L = wave_shr1(INT32_MAX, X1);
-        const bool i0 = Pex + c.cI0 > hp0, i1 = ex1 + c.cI1 > hp1;
-        const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
-        const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
-        const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
-        uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
-        uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
-        if (cold && __builtin_expect(np > 63u, 0)) {
-            // wide slot record of row r: u16 M / D slots per cell
-            reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
-                make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
-        }
-        // free-end candidates (SPEC.md §3.5) on H'
-        const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
-        int32_t e0 = X0 + eb;
-        int32_t e1 = X1 + eb;
-        if (FULL) {
-            e1 += (off == lim && lane == 63) ? 3 : 0;
-        } else {
-            if ((uint32_t)c.L2 == m - 1) e0 += 3;
-            if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
-            if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
-            if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
-        }
-        if (e0 > B.bE) B.bE = e0, B.bKey = r * 2, B.bOff = off;
-        if (e1 > B.bE) B.bE = e1, B.bKey = r * 2 + 1, B.bOff = off;
-        __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), B.rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u),
-                                              0, 0);
+        // decision bits, free-end candidates, record (only a cold row can
+        // have more than 63 predecessors)
+        row_record<FULL>(z, B.bE, B.bKey, B.bOff, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0,
+                         X1, Pex);
     };
     if (__builtin_expect(fast, 1)) {
         // the only predecessor is row r - 1 (tag 1), band moved by 0 or 1:
