@@ -312,3 +312,13 @@ def test_solo_config_hbm_read_instance(engine, mode):
         assert engine.kernel_cfg() == 3
     finally:
         engine.set_kernel_cfg(-1)
+
+
+def test_large_slice_picks_solo(engine):
+    """A slice of several times the occupancy object's resident ZMWs takes
+    the solo object by default (ccsx_gpu.cpp stage_slot) and stays byte-equal
+    to the oracle: 4,096 short ZMWs (300 bp x 6 passes)."""
+    zs = [synth(80000 + h, 300, 6) for h in range(4096)]
+    engine.set_kernel_cfg(-1)
+    _check(engine, zs, cx.MODE_SHRED, threads=16)
+    assert engine.kernel_cfg() == 3
