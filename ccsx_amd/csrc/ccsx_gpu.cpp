@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ccsx_layout.h"
@@ -476,16 +477,33 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
     uint8_t *hseq = s.h_seq.p;
     s.hoff.resize(nseg);
     s.hlen.resize(nseg);
-    for (size_t i = 0; i < nz; ++i) {
-        const ccsx_zmw_in &zi = z[i];
-        const ccsx::ZmwDesc &d = s.desc[i];
-        uint64_t hi = 0;
-        for (uint32_t k = 0; k < zi.nseg; ++k) {
-            s.hoff[d.seg0 + k] = zi.seg_off[k];
-            s.hlen[d.seg0 + k] = zi.seg_len[k];
-            hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
+    // the packing is a memory copy of the whole slice's subreads (1.8 GB for
+    // a 10k-ZMW config-E slice, ~100 ms on one thread): split over threads,
+    // since the slice's kernel cannot start before it is done (16,384-ZMW
+    // e2e line 17.3k -> 19.2k ZMWs/s, r03y).  Contexts sharing a device (the
+    // CLI's two per GPU) stage while the other's kernels run and keep to one
+    // thread, leaving the CPUs to the host pipeline's preparation.
+    auto pack = [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            const ccsx_zmw_in &zi = z[i];
+            const ccsx::ZmwDesc &d = s.desc[i];
+            uint64_t hi = 0;
+            for (uint32_t k = 0; k < zi.nseg; ++k) {
+                s.hoff[d.seg0 + k] = zi.seg_off[k];
+                s.hlen[d.seg0 + k] = zi.seg_len[k];
+                hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
+            }
+            if (hi) memcpy(hseq + d.seq_off, zi.seqs, hi);
         }
-        if (hi) memcpy(hseq + d.seq_off, zi.seqs, hi);
+    };
+    const size_t nthr = c->mem_share > 1 ? 1 : std::min<size_t>(std::min<size_t>(8, nz), std::max<uint64_t>(1, seq_b >> 27));
+    if (nthr <= 1) {
+        pack(0, nz);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t t = 1; t < nthr; ++t) th.emplace_back(pack, nz * t / nthr, nz * (t + 1) / nthr);
+        pack(0, nz / nthr);
+        for (auto &x : th) x.join();
     }
     HIPCHK(c, hipMemcpyAsync(s.d_seq.p, hseq, seq_b, hipMemcpyHostToDevice, s.stream));
     HIPCHK(c, hipMemcpyAsync(s.d_soff.p, s.hoff.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, s.stream));
@@ -740,6 +758,13 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
                     ms(std::chrono::steady_clock::now() - t_run).count());
         }
         const Pending &p = pend[si];
+        {
+            // one growth of the gathered CCS arena per slice, not one per
+            // ZMW's append (~150 MB for a 10k-ZMW config-E slice)
+            size_t add = 0;
+            for (size_t i = 0; i < s.nz; ++i) add += o[i].status ? 0 : o[i].len;
+            c->run_arena.reserve(c->run_arena.size() + add);
+        }
         for (size_t i = 0; i < s.nz; ++i) {
             const uint32_t g = (*p.idx)[p.b + i];
             out[g].cells = o[i].cells;
