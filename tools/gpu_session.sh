@@ -82,8 +82,8 @@ step() {
         echo "kt $cfg done" ;;
     pmc)
       timeout -k 10 900 bash "$R/tools/pmc_pass.sh" "$TAG/pmc_$cfg" --config "$cfg" > "$OUT/pmc_$cfg.log" 2>&1 && echo "pmc $cfg done" ;;
-    prof)
-      CFG=$cfg timeout -k 10 1000 bash "$R/tools/profile_gpu.sh" "${TAG}_$cfg" > "$OUT/prof_$cfg.log" 2>&1 && echo "prof $cfg done" ;;
+    prof)  # prof:CFG[:N] -- N ZMWs per GPU instead of the config's
+      CFG=$cfg NZMW=$k timeout -k 10 1000 bash "$R/tools/profile_gpu.sh" "${TAG}_$cfg${k:+_n$k}" > "$OUT/prof_$cfg.log" 2>&1 && echo "prof $cfg done" ;;
     phase)  # phase:L,PASSES,N:KCFG  (per-ZMW cycle split; CCSX_LIB=libccsx_amd_diag.so for the DP detail)
       local L P N; IFS=, read -r L P N <<< "$cfg"
       timeout -k 10 600 python -u tools/phase_prof.py --L "$L" --passes "$P" --n "$N" --kcfg "${k:--1}" \
