@@ -104,13 +104,18 @@ uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *ctx);
  * ZMWs of the last launch: total, read staging, DP, traceback, merge,
  * columns, breakpoint+emission, DP rows.  Off by default. */
 int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
-/* Test hook: tight row capacity override (0 = default 3 x longest segment + 4096). */
+/* Test hook: tight row capacity override (0 = default 3 x longest segment +
+ * 4096, the segment capped at the 4,096-base window read buffer in shredded
+ * mode). */
 int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
 /* Kernel configuration of the next slices: -1 (default) = by slice size (the
- * latency configuration -- three waves, 8-row DP blocks, 32-row LDS ring --
- * when it keeps the whole slice resident, else the occupancy one -- 4-row
- * blocks, 24-row ring, one more workgroup per CU); 0 / 1 / 2 force one (2:
- * the throughput configuration, two-wave workgroups, up to 8 per CU).
+ * latency configuration 0 -- three waves, 8-row DP blocks, 32-row LDS ring --
+ * when it keeps the whole slice resident; the solo configuration 3 -- one
+ * wave per ZMW, 8-row ring, 14-16 ZMWs per CU -- for slices of at least 3x
+ * what the occupancy one keeps resident; else the occupancy configuration 1
+ * -- 4-row blocks, 24-row ring, one more workgroup per CU); 0 / 1 / 2 / 3
+ * force one (2: the throughput configuration, two-wave workgroups, up to 8
+ * per CU, only by this call).
  * ccsx_gpu_kernel_cfg: the configuration of the last staged slice. */
 int ccsx_gpu_set_kernel_cfg(ccsx_ctx *ctx, int cfg);
 int ccsx_gpu_kernel_cfg(const ccsx_ctx *ctx);
