@@ -185,8 +185,9 @@ struct ccsx_ctx {
     std::string err;
     Slot slot[2];
     int32_t cfg_force = -1;            // test hook: -1 = by slice size
-    uint32_t wg_cap = 0;               // measurement hook (CCSX_WG_PER_CU): LDS request padded to cap workgroups per CU
-    // LDS read buffer of tight-cap shredded slices, bases (CCSX_SHRED_READ_CAP):
+    uint32_t wg_cap = 0;               // measurement hook (ccsx_gpu_set_wg_cap): LDS request padded to cap workgroups per CU
+    uint64_t slot_budget = 0;          // test hook (ccsx_gpu_set_slot_budget): bytes per slot, 0 = by device memory
+    // LDS read buffer of tight-cap shredded slices, bases (ccsx_gpu_set_shred_read_cap):
     // pushed windows are 2-3 kb unless a breakpoint is missed (+2 kb each,
     // main.c:552-570); a longer one fails the ZMW with kErrReadLen and
     // ccsx_gpu_run re-runs it uncapped.  4,096 rather than 8,192 bases: 2 KB
@@ -195,6 +196,8 @@ struct ccsx_ctx {
     uint32_t shred_read_cap = 4096;
     uint32_t ncu = 256;                // compute units of the device
     uint64_t reruns = 0;               // ZMWs ccsx_gpu_run re-ran with full caps
+    uint64_t slices = 0;               // slices ccsx_gpu_run launched
+    uint64_t dealt = 0, parts = 0;     // lists ccsx_gpu_run dealt into interleaved parts, and their parts
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
     int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
@@ -246,21 +249,6 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
         int n = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0)
             c->ncu = (uint32_t)n;
-    }
-    // CCSX_KCFG forces a kernel configuration (A/B runs of the CLI / e2e)
-    if (const char *k = getenv("CCSX_KCFG")) {
-        const int v = atoi(k);
-        if (v >= -1 && v < ccsx::kCfgCount) c->cfg_force = v;
-    }
-    // CCSX_WG_PER_CU caps the resident workgroups per CU by padding the LDS
-    // request (the residency curve of DESIGN.md section 5; never the default)
-    if (const char *k = getenv("CCSX_WG_PER_CU")) {
-        const int v = atoi(k);
-        if (v > 0 && v <= 16) c->wg_cap = (uint32_t)v;
-    }
-    if (const char *k = getenv("CCSX_SHRED_READ_CAP")) {
-        const int v = atoi(k);
-        if (v >= 1024 && v <= 65536) c->shred_read_cap = (uint32_t)v;
     }
     if (e != hipSuccess) {
         fprintf(stderr, "[ccsx_gpu] cannot open device %d: %s\n", device, hipGetErrorString(e));
@@ -715,7 +703,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
     }
     // two slots in flight: each holds half
-    const uint64_t slot_budget = std::max<uint64_t>(1ull << 29, budget / 2);
+    const uint64_t slot_budget = c->slot_budget ? c->slot_budget : std::max<uint64_t>(1ull << 29, budget / 2);
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     using ms = std::chrono::duration<double, std::milli>;
     const auto t_run = std::chrono::steady_clock::now();
@@ -797,34 +785,51 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     std::vector<ccsx_zmw_in> sub;
     std::vector<uint32_t> inter;  // run_list's interleaved order (lives until its slots are collected)
     auto run_list = [&](const std::vector<uint32_t> &idx0, bool full, std::vector<uint32_t> *retry) -> int {
-        // A list of one launch class that needs both slots but no more is cut
-        // into two interleaved halves (cost ranks 0, 2, 4, ... and 1, 3, 5,
-        // ..., each still most expensive first) instead of the most expensive
-        // half and the cheapest: the two kernels run side by side, so each
-        // now ends on cheap ZMWs and they end together, where the contiguous
-        // cut left the expensive slice running alone with a sparse tail
-        // (16,384 config-E ZMWs: the 5,671 cheap ones done after 180 ms, the
-        // other 10,713 after 737 ms; one launch of all of them: 698 ms).
+        // A list of one launch class that needs k > 1 slots is dealt into k
+        // interleaved parts (cost rank i goes to part i % k, each part still
+        // most expensive first) instead of being cut into contiguous runs of
+        // the cost order: consecutive parts run side by side on the two
+        // slots and each ends on cheap ZMWs, so they end together and no
+        // slice is a small tail of the cheapest ZMWs (a latency-object
+        // launch), nor the most expensive ones running alone with a sparse
+        // tail (16,384 config-E ZMWs cut contiguously: the 5,671 cheap ones
+        // done after 180 ms, the other 10,713 after 737 ms; one launch of
+        // all of them: 698 ms).  k grows until every part fits a slot.
         const std::vector<uint32_t> *lp = &idx0;
-        size_t cut = SIZE_MAX;
-        if (!idx0.empty() && cls[idx0.front()] == cls[idx0.back()]) {
-            uint64_t tot = 0, ha = 0, hb = 0;
+        std::vector<size_t> cuts;  // part boundaries in *lp
+        bool one_class = !idx0.empty();
+        for (uint32_t g : idx0) one_class = one_class && cls[g] == cls[idx0.front()];
+        if (one_class) {
+            std::vector<uint64_t> xb(idx0.size());
+            uint64_t tot = 0, xmax = 0;
             for (size_t i = 0; i < idx0.size(); ++i) {
-                const uint64_t x = zmw_bytes(z[idx0[i]], full, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
-                tot += x;
-                (i & 1 ? hb : ha) += x;
+                xb[i] = zmw_bytes(z[idx0[i]], full, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+                tot += xb[i];
+                xmax = std::max(xmax, xb[i]);
             }
-            if (tot > slot_budget && ha <= slot_budget && hb <= slot_budget) {
-                inter.clear();
-                for (size_t i = 0; i < idx0.size(); i += 2) inter.push_back(idx0[i]);
-                cut = inter.size();
-                for (size_t i = 1; i < idx0.size(); i += 2) inter.push_back(idx0[i]);
-                lp = &inter;
+            if (tot > slot_budget && xmax <= slot_budget) {
+                const size_t k0 = size_t((tot + slot_budget - 1) / slot_budget);
+                for (size_t k = k0; k <= std::min<size_t>(idx0.size(), k0 + 8); ++k) {
+                    std::vector<uint64_t> part(k, 0);
+                    for (size_t i = 0; i < idx0.size(); ++i) part[i % k] += xb[i];
+                    if (*std::max_element(part.begin(), part.end()) > slot_budget) continue;
+                    inter.clear();
+                    for (size_t p = 0; p < k; ++p) {
+                        if (p) cuts.push_back(inter.size());
+                        for (size_t i = p; i < idx0.size(); i += k) inter.push_back(idx0[i]);
+                    }
+                    lp = &inter;
+                    ++c->dealt;
+                    c->parts += k;
+                    break;
+                }
             }
         }
         const std::vector<uint32_t> &idx = *lp;
-        size_t b = 0;
+        size_t b = 0, ci = 0;
         while (b < idx.size()) {
+            while (ci < cuts.size() && cuts[ci] <= b) ++ci;
+            const size_t cut = ci < cuts.size() ? cuts[ci] : SIZE_MAX;
             uint64_t need = 0;
             size_t e = b;
             while (e < idx.size()) {
@@ -847,6 +852,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             if (r) return r;
             r = launch_slot(c, c->slot[si], mode);
             if (r) return r;
+            ++c->slices;
             b = e;
         }
         // both slots' results before the list's vectors go away
@@ -868,6 +874,11 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     int r = run_list(all, false, &retry);
     if (!r && !retry.empty()) {
         for (uint32_t g : retry) cls[g] = zmw_class(z[g], false);  // full caps: whole segments in the buffer
+        // the tight pass had them all in class 0: regroup by the new classes
+        // (most expensive first within each), so a slice never ends at every
+        // class change of an alternating list
+        std::stable_sort(retry.begin(), retry.end(),
+                         [&](uint32_t x, uint32_t y) { return cls[x] != cls[y] ? cls[x] < cls[y] : cost[x] > cost[y]; });
         if (timing) fprintf(stderr, "[ccsx_gpu_run] dev %d: %zu ZMWs re-run with full caps\n", c->device, retry.size());
         c->reruns += retry.size();
         r = run_list(retry, true, nullptr);
@@ -909,10 +920,45 @@ int ccsx_gpu_kernel_cfg(const ccsx_ctx *c) { return c ? c->slot[0].cfg : -1; }
 
 int64_t ccsx_gpu_rerun_count(const ccsx_ctx *c) { return c ? (int64_t)c->reruns : -1; }
 
+int ccsx_gpu_run_stats(const ccsx_ctx *c, uint64_t *st, uint32_t n)
+{
+    if (!c || !st) return -1;
+    const uint64_t v[4] = {c->reruns, c->slices, c->dealt, c->parts};
+    for (uint32_t i = 0; i < n && i < 4; ++i) st[i] = v[i];
+    return 0;
+}
+
+uint64_t ccsx_gpu_zmw_bytes(const ccsx_ctx *c, int mode, const ccsx_zmw_in *z)
+{
+    if (!c || !z) return 0;
+    return zmw_bytes(*z, false, c->tight_rows, mode == CCSX_MODE_SHRED ? c->shred_read_cap : 0u);
+}
+
 int ccsx_gpu_set_fault(ccsx_ctx *c, int64_t zmw)
 {
     if (!c) return -1;
     c->fault = zmw;
+    return 0;
+}
+
+int ccsx_gpu_set_slot_budget(ccsx_ctx *c, uint64_t bytes)
+{
+    if (!c) return -1;
+    c->slot_budget = bytes;
+    return 0;
+}
+
+int ccsx_gpu_set_wg_cap(ccsx_ctx *c, uint32_t wg_per_cu)
+{
+    if (!c || wg_per_cu > 16) return -1;
+    c->wg_cap = wg_per_cu;
+    return 0;
+}
+
+int ccsx_gpu_set_shred_read_cap(ccsx_ctx *c, uint32_t bases)
+{
+    if (!c || bases < 1024 || bases > 65536) return -1;
+    c->shred_read_cap = bases;
     return 0;
 }
 

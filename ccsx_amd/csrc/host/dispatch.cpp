@@ -3,11 +3,14 @@
 //
 // The reference balances ZMWs over its CPU threads dynamically: kt_for deals
 // indices round-robin and idle threads steal (kthread.c:24-46).  A GPU launch
-// is only efficient with ~1,000+ ZMWs in it, so here the unit a device context
-// pulls is a micro-batch: the chunk's ZMWs in longest-processing-time order
-// (largest estimated cost first), cut into consecutive runs of about equal
-// cost.  Contexts pull batches in that order, so the expensive ZMWs start
-// first and a chunk ends on batches of small ones.
+// is only efficient with thousands of ZMWs in it, so here the unit a device
+// context pulls is a micro-batch: the chunk's ZMWs ranked by estimated cost
+// (largest first) and the ranks dealt round-robin over the batches, kt_for's
+// dealing applied to cost ranks.  Every batch then holds the same mix of
+// expensive and cheap ZMWs (batch costs differ by at most one ZMW's cost), so
+// no batch is only a chunk's most expensive ZMWs -- whose launch would end
+// on its slowest serial chains -- and each launch, ordered longest first on
+// the device, ends on cheap ones.
 #include <algorithm>
 #include <numeric>
 #include <vector>
@@ -32,27 +35,19 @@ uint32_t ccsx_partition(const uint64_t *cost, uint32_t n, uint32_t nparts, uint3
         bounds[0] = 0;
         return 0;
     }
-    for (uint32_t i = 0; i < n; ++i) order[i] = i;
-    // LPT order; equal costs keep input order (deterministic batches)
-    std::stable_sort(order, order + n, [cost](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    std::vector<uint32_t> rank(n);
+    for (uint32_t i = 0; i < n; ++i) rank[i] = i;
+    // LPT ranks; equal costs keep input order (deterministic batches)
+    std::stable_sort(rank.begin(), rank.end(), [cost](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
     if (nparts < 1) nparts = 1;
     if (min_batch < 1) min_batch = 1;
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i) total += cost[i];
-    const uint64_t target = (total + nparts - 1) / nparts;
-    uint32_t nb = 0, start = 0;
-    uint64_t acc = 0;
-    bounds[nb++] = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        acc += cost[order[i]];
-        const uint32_t cnt = i + 1 - start, rest = n - (i + 1);
-        // cut once the batch holds its share, but never leave a batch (this
-        // one or the remainder) below min_batch ZMWs
-        if (rest > 0 && acc >= target && cnt >= min_batch && rest >= min_batch) {
-            bounds[nb++] = i + 1;
-            start = i + 1;
-            acc = 0;
-        }
+    // as many batches as asked, none below min_batch ZMWs (one if n is short)
+    const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(nparts, n / min_batch));
+    // batch b = ranks b, b + nb, b + 2 nb, ...: contiguous in `order`
+    uint32_t o = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        bounds[b] = o;
+        for (uint32_t r = b; r < n; r += nb) order[o++] = rank[r];
     }
     bounds[nb] = n;
     return nb;

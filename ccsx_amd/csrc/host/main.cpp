@@ -16,6 +16,7 @@
 //     back (main.c:707-717).
 // A ZMW the device cannot finish is reported on stderr and skipped; the other
 // ZMWs of the run are written (the reference has no per-ZMW failure).
+#include <errno.h>
 #include <getopt.h>
 
 #include <algorithm>
@@ -86,9 +87,10 @@ int usage()
             "               GPUs places group g on GPU g %% visible (logical contexts)\n"
             "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
-            "CCSX_CHUNK     Largest chunk in ZMWs [16384 x min(groups, 4)]\n"
+            "CCSX_CHUNK     Largest chunk in ZMWs [8192 x contexts]\n"
             "CCSX_CHUNK0    First chunk in ZMWs [1024], growing x4 up to CCSX_CHUNK\n"
             "CCSX_KCFG      Force a kernel configuration (0 latency, 1 occupancy, 2 throughput, 3 solo)\n"
+            "CCSX_DEV_SHARE Processes sharing each GPU [1] (each context's memory share shrinks)\n"
             "\n"
             "Arguments:\n"
             "input          Input file.\n"
@@ -396,12 +398,26 @@ int main(int argc, char **argv)
     std::vector<ccsx_ctx *> ctx(nctx, nullptr);
     std::vector<int> per_dev(ndev, 0);
     for (int i = 0; i < nctx; ++i) per_dev[(i / nslot) % ndev]++;
+    // processes sharing each device (bench.py's multi-rank rehearsal on one
+    // GPU): each context's memory share shrinks by that factor
+    int dev_share = 1;
+    if (const char *e = getenv("CCSX_DEV_SHARE")) dev_share = std::max(1, std::min(64, atoi(e)));
+    // measurement overrides of the engine (never set by default)
+    const int kcfg = getenv("CCSX_KCFG") ? atoi(getenv("CCSX_KCFG")) : -1;
+    const int wg_cap = getenv("CCSX_WG_PER_CU") ? atoi(getenv("CCSX_WG_PER_CU")) : 0;
+    const int read_cap = getenv("CCSX_SHRED_READ_CAP") ? atoi(getenv("CCSX_SHRED_READ_CAP")) : 0;
     for (int i = 0; i < nctx; ++i) {
         const int dev = (i / nslot) % ndev;
         if (ccsx_gpu_open(dev, &ctx[i]) != 0) return 1;
-        ccsx_gpu_set_mem_share(ctx[i], (uint32_t)per_dev[dev]);
+        ccsx_gpu_set_mem_share(ctx[i], (uint32_t)(per_dev[dev] * dev_share));
         ccsx_gpu_set_prealloc(ctx[i], 1);
         if (verbose > 2 && split_subread) ccsx_gpu_set_bp_log(ctx[i], 1);
+        if ((kcfg >= 0 && ccsx_gpu_set_kernel_cfg(ctx[i], kcfg) != 0) ||
+            (wg_cap > 0 && ccsx_gpu_set_wg_cap(ctx[i], (uint32_t)wg_cap) != 0) ||
+            (read_cap > 0 && ccsx_gpu_set_shred_read_cap(ctx[i], (uint32_t)read_cap) != 0)) {
+            fprintf(stderr, "[ccsx] invalid CCSX_KCFG / CCSX_WG_PER_CU / CCSX_SHRED_READ_CAP\n");
+            return 1;
+        }
     }
 
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
@@ -417,6 +433,7 @@ int main(int argc, char **argv)
     BatchQueue queue;
     ChunkRing ring(3);
     std::atomic<bool> fatal(false);
+    std::atomic<uint64_t> cells_total(0);  // DP cells the devices computed (CCSX_TIMING report)
     std::mutex err_m;
 
     // test hook: the device reports this hole as failed (tests/test_gpu_cli.py)
@@ -441,6 +458,9 @@ int main(int argc, char **argv)
                 const int r = ccsx_gpu_run(ctx[w], mode, in.data(), in.size(), out.data());
                 if (r == 0 || r == -2) {
                     // -2: some ZMWs failed on the device, the rest are valid
+                    uint64_t cells = 0;
+                    for (size_t i = 0; i < b.idx.size(); ++i) cells += out[i].cells;
+                    cells_total += cells;
                     for (size_t i = 0; i < b.idx.size(); ++i) {
                         Zmw &z = ch.zs[b.idx[i]];
                         z.status = out[i].status;
@@ -504,14 +524,17 @@ int main(int argc, char **argv)
 
     // step 0 (main.c:652-697) + the CPU half of step 1; the reference grows
     // the chunk 1,024 -> 4,096 -> 16,384 ZMWs (main.c:686-690), here the
-    // last size scales with the devices (output order does not depend on it)
-    // micro-batches per context and chunk (CCSX_CTX_BATCHES, default 1: a
-    // context's batch of a 16,384-ZMW chunk is then large enough for the
-    // solo kernel configuration; 100k config-E ZMWs from the generator's
-    // pipe 15.2 s with 2, 11.8 s with 1, r03o)
+    // last size scales with the device contexts (output order does not
+    // depend on it): 8,192 ZMWs per context, so that each context's batch,
+    // cut into its two slots' slices, still holds ~4,096 ZMWs per launch --
+    // above the solo configuration's threshold (3 x the occupancy object's
+    // resident ZMWs, 3,840 on config E) -- also with 8 GPUs x 2 contexts.
+    // micro-batches per context and chunk (CCSX_CTX_BATCHES, default 1: 100k
+    // config-E ZMWs from the generator's pipe 15.2 s with 2, 11.8 s with 1,
+    // r03o)
     uint32_t batches_per_ctx = 1;
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    size_t chunk_max = 16384u * (size_t)std::min(ngroup, 4);
+    size_t chunk_max = std::min<size_t>(8192u * (size_t)nctx, 262144u);
     if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));
     // step 0's reading on its own thread, one chunk ahead of the preparation
     // (the reference's step 0 does both in turn: main.c:652-697)
@@ -557,7 +580,8 @@ int main(int argc, char **argv)
         const size_t id = ch->id;
         const double t0 = ch->t_read0, t1 = ch->t_read1;
         prepare_chunk(zs, nthreads, verbose);
-        // cost-balanced micro-batches, longest first (dispatch.cpp)
+        // cost-balanced micro-batches: cost ranks dealt round-robin, each
+        // batch longest first (dispatch.cpp)
         const uint32_t n = (uint32_t)zs.size();
         std::vector<uint64_t> cost(n);
         for (uint32_t i = 0; i < n; ++i) cost[i] = ccsx_zmw_cost(zs[i].seg_len.data(), (uint32_t)zs[i].seg_len.size());
@@ -591,18 +615,22 @@ int main(int argc, char **argv)
         // every byte is written: flush and leave without tearing down the
         // device contexts (≈ 0.8 s of hipFree / hipHostFree for a 100k run)
         // or the last chunk; process exit releases both
-        if (fp_out != stdout) fclose(fp_out);
-        fflush(stdout);  // (-v >= 3 breakpoint lines go to stdout)
-        if (timing) fprintf(stderr, "[ccsx] output done at %.0f ms\n", tw);
+        // a failed final write (ENOSPC, EPIPE on a FIFO) must not exit 0
+        bool werr = fp_out != stdout && (ferror(fp_out) || fclose(fp_out) != 0);
+        werr = (ferror(stdout) || fflush(stdout) != 0) || werr;  // (-v >= 3 breakpoint lines go to stdout)
+        if (werr) fprintf(stderr, "[ccsx] error writing the output: %s\n", strerror(errno));
+        if (timing)
+            fprintf(stderr, "[ccsx] output done at %.0f ms; device cells %llu\n", tw,
+                    (unsigned long long)cells_total.load());
         if (nfail) fprintf(stderr, "[ccsx] %zu ZMWs had no CCS (device status, see above)\n", nfail);
         fflush(stderr);
-        std::_Exit(0);
+        std::_Exit(werr ? 1 : 0);
     }
     for (auto *x : ctx) ccsx_gpu_close(x);
     if (timing) fprintf(stderr, "[ccsx] output done at %.0f ms, contexts closed at %.0f ms\n", tw, now_ms());
     rd.reset();
-    if (fp_out != stdout) fclose(fp_out);
-    else fflush(stdout);
+    if (fp_out != stdout) (void)fclose(fp_out);
+    else (void)fflush(stdout);
     if (nfail) fprintf(stderr, "[ccsx] %zu ZMWs had no CCS (device status, see above)\n", nfail);
     return fatal ? 1 : 0;
 }

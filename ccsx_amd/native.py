@@ -26,7 +26,9 @@ EXPORTS = {
                    "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows",
                    "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault",
                    "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count",
-                   "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for"],
+                   "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for",
+                   "ccsx_gpu_run_stats", "ccsx_gpu_zmw_bytes", "ccsx_gpu_set_slot_budget", "ccsx_gpu_set_wg_cap",
+                   "ccsx_gpu_set_shred_read_cap"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
                     "ccsx_zmw_cost", "ccsx_partition",
@@ -79,6 +81,16 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_kernel_cfg.argtypes = [C.c_void_p]
         L.ccsx_gpu_rerun_count.argtypes = [C.c_void_p]
         L.ccsx_gpu_rerun_count.restype = C.c_int64
+        L.ccsx_gpu_run_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]
+        L.ccsx_gpu_zmw_bytes.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwIn)]
+        L.ccsx_gpu_zmw_bytes.restype = C.c_uint64
+        L.ccsx_gpu_set_slot_budget.argtypes = [C.c_void_p, C.c_uint64]
+        L.ccsx_gpu_set_wg_cap.argtypes = [C.c_void_p, C.c_uint32]
+        L.ccsx_gpu_set_shred_read_cap.argtypes = [C.c_void_p, C.c_uint32]
+        L.ccsx_gpu_set_mem_share.argtypes = [C.c_void_p, C.c_uint32]
+        L.ccsx_gpu_set_bp_log.argtypes = [C.c_void_p, C.c_int]
+        L.ccsx_gpu_bp_log.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.POINTER(C.c_uint32)),
+                                      C.POINTER(C.c_uint32)]
         L.ccsx_revcomp.argtypes = [C.c_char_p, C.c_uint32]
         L.ccsx_prepare.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]
@@ -342,13 +354,24 @@ class Engine:
         return [(C.string_at(out[i].ccs, out[i].len) if out[i].len else b"", out[i].status, out[i].cells)
                 for i in range(len(zmws))]
 
-    def run_batch(self, batch: "SynthBatch", mode: int = MODE_SHRED):
-        """ccsx_gpu_run on a synthetic batch; returns [(status, cells)] (no CCS copy)."""
+    def run_batch(self, batch: "SynthBatch", mode: int = MODE_SHRED, keep=()):
+        """ccsx_gpu_run on a synthetic batch; returns [(status, cells, len)]
+        and, when `keep` lists batch indices, also {index: CCS bytes}."""
         out = (ZmwOut * max(batch.n, 1))()
         rc = self._L.ccsx_gpu_run(self._ctx, mode, batch.zmws, batch.n, out)
         if rc != 0:
             self._err("ccsx_gpu_run")
-        return [(out[i].status, out[i].cells, out[i].len) for i in range(batch.n)]
+        res = [(out[i].status, out[i].cells, out[i].len) for i in range(batch.n)]
+        if keep:
+            return res, {i: C.string_at(out[i].ccs, out[i].len) if out[i].len else b"" for i in keep}
+        return res
+
+    def stage_batch(self, batch: "SynthBatch", mode: int = MODE_SHRED) -> None:
+        """ccsx_gpu_stage_for on a synthetic batch (inputs resident for launch())."""
+        if self._L.ccsx_gpu_stage_for(self._ctx, mode, batch.zmws, batch.n) != 0:
+            self._err("ccsx_gpu_stage_for")
+        self._keep = batch
+        self._nz = batch.n
 
     def set_mem_share(self, share: int) -> None:
         """This context uses at most 1/share of the device's memory (several
@@ -367,6 +390,46 @@ class Engine:
     def rerun_count(self) -> int:
         """ZMWs run() has re-run with full caps so far."""
         return int(self._L.ccsx_gpu_rerun_count(self._ctx))
+
+    def run_stats(self) -> dict:
+        """ccsx_gpu_run counters so far: reruns, slices, dealt lists, their parts."""
+        st = (C.c_uint64 * 4)()
+        if self._L.ccsx_gpu_run_stats(self._ctx, st, 4) != 0:
+            self._err("ccsx_gpu_run_stats")
+        return dict(zip(("reruns", "slices", "dealt", "parts"), (int(x) for x in st)))
+
+    def zmw_bytes(self, z: Prepared, mode: int = MODE_SHRED) -> int:
+        """Device bytes one ZMW occupies in a ccsx_gpu_run slice of `mode`."""
+        arr, keep = self._build_in([z])
+        return int(self._L.ccsx_gpu_zmw_bytes(self._ctx, mode, arr))
+
+    def set_bp_log(self, on: bool = True) -> None:
+        """Record the -v >= 3 breakpoint log (main.c:619-620) in ccsx_gpu_run."""
+        if self._L.ccsx_gpu_set_bp_log(self._ctx, 1 if on else 0) != 0:
+            self._err("ccsx_gpu_set_bp_log")
+
+    def bp_log(self, i: int) -> list:
+        """(breakpoint, MSA columns) per shredding round of ZMW i of the last run()."""
+        pr = C.POINTER(C.c_uint32)()
+        n = C.c_uint32(0)
+        if self._L.ccsx_gpu_bp_log(self._ctx, i, C.byref(pr), C.byref(n)) != 0:
+            self._err("ccsx_gpu_bp_log")
+        return [(int(pr[2 * r]), int(pr[2 * r + 1])) for r in range(n.value)]
+
+    def set_slot_budget(self, nbytes: int) -> None:
+        """Test hook: bytes per ccsx_gpu_run slot (0 = by device memory)."""
+        if self._L.ccsx_gpu_set_slot_budget(self._ctx, nbytes) != 0:
+            self._err("ccsx_gpu_set_slot_budget")
+
+    def set_wg_cap(self, wg_per_cu: int) -> None:
+        """Measurement hook: at most wg_per_cu resident workgroups per CU (0 = off)."""
+        if self._L.ccsx_gpu_set_wg_cap(self._ctx, wg_per_cu) != 0:
+            self._err("ccsx_gpu_set_wg_cap")
+
+    def set_shred_read_cap(self, bases: int) -> None:
+        """The LDS read buffer of tight-cap shredded slices, in bases."""
+        if self._L.ccsx_gpu_set_shred_read_cap(self._ctx, bases) != 0:
+            self._err("ccsx_gpu_set_shred_read_cap")
 
     def set_tight_rows(self, rows: int) -> None:
         """Test hook: override the tight row capacity (0 = default)."""

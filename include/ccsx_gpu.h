@@ -121,6 +121,25 @@ int ccsx_gpu_set_kernel_cfg(ccsx_ctx *ctx, int cfg);
 int ccsx_gpu_kernel_cfg(const ccsx_ctx *ctx);
 /* ZMWs ccsx_gpu_run has re-run with full caps on this context so far. */
 int64_t ccsx_gpu_rerun_count(const ccsx_ctx *ctx);
+/* Counters of this context's ccsx_gpu_run calls so far, the first n of:
+ * [0] ZMWs re-run with full caps, [1] slices launched, [2] ZMW lists dealt
+ * into interleaved parts (a list of one launch class that needs k > 1 slots),
+ * [3] the parts of those lists. */
+int ccsx_gpu_run_stats(const ccsx_ctx *ctx, uint64_t *stats, uint32_t n);
+/* Device bytes ZMW *z occupies in a ccsx_gpu_run slice of `mode` (tight
+ * capacities: workspace, subreads, output slab, tables). */
+uint64_t ccsx_gpu_zmw_bytes(const ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z);
+/* Test hook: bytes per slot for ccsx_gpu_run's slices (0 = by device memory:
+ * half of this context's share, ccsx_gpu_set_mem_share), so a small batch is
+ * cut into several slices. */
+int ccsx_gpu_set_slot_budget(ccsx_ctx *ctx, uint64_t bytes);
+/* Measurement hooks (the host program maps CCSX_WG_PER_CU / CCSX_SHRED_READ_CAP
+ * onto them): pad the LDS request so at most wg_per_cu workgroups share a CU
+ * (0 = off); the LDS read buffer of tight-cap shredded slices in bases
+ * (1,024-65,536, default 4,096; a longer pushed window re-runs the ZMW with
+ * full caps). */
+int ccsx_gpu_set_wg_cap(ccsx_ctx *ctx, uint32_t wg_per_cu);
+int ccsx_gpu_set_shred_read_cap(ccsx_ctx *ctx, uint32_t bases);
 /* Test hook: the next ccsx_gpu_run reports ZMW `zmw` (index into its batch)
  * as failed (status 8) after computing it, as a device failure would; the
  * run returns -2 and the other ZMWs are valid.  -1 = off. */

@@ -44,11 +44,11 @@ ccsx_pairaln ccsx_pairwise(const uint8_t *q, uint32_t qlen, const uint8_t *t, ui
  * ZMW indices over threads, kthread.c:24-46).
  * ccsx_zmw_cost: estimated POA work of one prepared ZMW, S x (28 + nseg) with
  * S = sum of segment lengths.
- * ccsx_partition: order[n] = the ZMWs by decreasing cost (ties in input
- * order); bounds[0..nb] = batch b is order[bounds[b] .. bounds[b+1]).  Batches
- * are consecutive runs of about total / nparts cost, none (except a lone one)
- * below min_batch ZMWs.  bounds needs room for n + 1 entries (nb <= n).
- * Returns nb. */
+ * ccsx_partition: nb = min(nparts, n / min_batch) batches (at least one);
+ * the ZMWs ranked by decreasing cost (ties in input order) and rank r dealt to
+ * batch r % nb, so batch costs differ by at most one ZMW's cost.  Batch b is
+ * order[bounds[b] .. bounds[b+1]), in decreasing cost.  bounds needs room for
+ * n + 1 entries.  Returns nb. */
 uint64_t ccsx_zmw_cost(const uint32_t *seg_len, uint32_t nseg);
 uint32_t ccsx_partition(const uint64_t *cost, uint32_t n, uint32_t nparts, uint32_t min_batch,
                         uint32_t *order, uint32_t *bounds);

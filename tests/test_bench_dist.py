@@ -73,8 +73,11 @@ def test_bench_two_ranks_on_device():
     """The driver's N > 1 launch (torch.distributed.run, one process per rank,
     RANK/LOCAL_RANK/WORLD_SIZE from the env) with both ranks on the box's one
     GPU: per-rank hole ranges, barrier, max-over-ranks time, summed cells, one
-    JSON line, and the e2e line's gather."""
-    small = ["--steps", "2", "--warmup", "1", "--nzmw", "96", "--e2e-zmws", "64", "--no-cpu-baseline"]
+    JSON line; the config-E headline split over the ranks' CLIs (each over
+    its own hole range, its device share halved) with the sample checked
+    against the oracle; the e2e line's gather."""
+    small = ["--steps", "2", "--warmup", "1", "--nzmw", "96", "--e2e-zmws", "64", "--no-cpu-baseline",
+             "--e-zmws", "600", "--e-sample", "12", "--roofline-zmws", "128"]
     one = _run_bench(1, small)
     two = _run_bench(2, small)
     import ccsx_amd.native as nat
@@ -89,6 +92,21 @@ def test_bench_two_ranks_on_device():
         assert "ranks_per_device" not in two["config"]
     # rank 1 aligns its own 96 holes: the summed cells are two ranks' worth,
     # and the two ranks' cell counts differ (disjoint synthetic holes)
-    assert two["cells_per_step"] > one["cells_per_step"]
-    assert two["cells_per_step"] != 2 * one["cells_per_step"]
+    k1, k2 = one["kernel_B"], two["kernel_B"]
+    assert k2["cells_per_step"] > k1["cells_per_step"]
+    assert k2["cells_per_step"] != 2 * k1["cells_per_step"]
+    # the headline: 600 config-E ZMWs in both runs, rank 0's 300 in order
+    assert one["cli"]["zmws"] == 600 and two["cli"]["zmws"] == 300
+    assert one["cli"]["sample_equal"] == one["cli"]["sample"] == 12
+    assert two["cli"]["sample_equal"] == two["cli"]["sample"] == 12
     assert two["value"] > 0 and two["e2e"]["value"] > 0
+    assert two["e2e"]["sample_equal"] == two["e2e"]["sample"] == 64
+    assert one["roofline"]["kernel_cfg"] in (0, 1, 3) and one["scaling"] == "strong"
+
+
+def test_e_rank_ranges_split_the_config():
+    for world in (1, 2, 3, 8):
+        rs = [bench.e_rank_range(500_000, r, world) for r in range(world)]
+        assert sum(len(r) for r in rs) == 500_000
+        assert all(a.stop == b.start for a, b in zip(rs, rs[1:]))
+        assert rs[0].start == bench.E_HOLE0 and max(map(len, rs)) - min(map(len, rs)) <= 1

@@ -322,3 +322,50 @@ def test_large_slice_picks_solo(engine):
     engine.set_kernel_cfg(-1)
     _check(engine, zs, cx.MODE_SHRED, threads=16)
     assert engine.kernel_cfg() == 3
+
+
+def _e_zmws(hole0, n):
+    import bench
+    cfg = bench.CONFIGS["E"]
+    return [cx.prepare(cx.synth_zmw(bench.SEED, h, *bench.zmw_shape(cfg, h))[0]) for h in range(hole0, hole0 + n)]
+
+
+def test_multi_slice_run(engine):
+    """ccsx_gpu_run's multi-slice paths under a small slot budget
+    (ccsx_gpu_set_slot_budget): ~150 config-E ZMWs dealt into >= 4
+    interleaved parts on the two slots, two ZMWs whose pushed window outgrows
+    the 4,096-base read cap (kErrReadLen, re-run with full caps after the
+    pipelined slices), the -v >= 3 breakpoint log gathered across slots; then
+    a budget below the largest ZMW, so the list is cut into contiguous
+    slices.  CCS, input order and the breakpoint log byte-equal to the
+    oracle."""
+    from oracle.oracle import Poa
+    zs = _e_zmws(10_500_000, 150)
+    zs.insert(70, synth(7500, 12000, 2))
+    zs.insert(20, synth(7502, 9000, 2))
+    tot = sum(engine.zmw_bytes(z) for z in zs)
+    st0 = engine.run_stats()
+    engine.set_slot_budget(int(tot / 3.5))
+    engine.set_bp_log(True)
+    try:
+        _check(engine, zs, cx.MODE_SHRED, threads=16)
+        st = engine.run_stats()
+        assert st["dealt"] - st0["dealt"] >= 1
+        assert st["parts"] - st0["parts"] >= 4
+        assert st["reruns"] - st0["reruns"] >= 2
+        assert st["slices"] - st0["slices"] >= 6  # >= 4 parts + the re-run
+        ref = Poa()
+        for i in (0, 20, 21, 70, 71, len(zs) - 1):
+            _, bps = ref.zmw_breakpoints(zs[i].seqs, zs[i].offs, zs[i].lens)
+            assert engine.bp_log(i) == [tuple(x) for x in bps], f"ZMW {i}: breakpoint log"
+        # contiguous slices: a budget below the largest ZMW of the list
+        small = zs[:24]
+        sizes = sorted(engine.zmw_bytes(z) for z in small)
+        engine.set_slot_budget(sizes[-2])
+        st0 = engine.run_stats()
+        _check(engine, small, cx.MODE_SHRED, threads=16)
+        st = engine.run_stats()
+        assert st["dealt"] == st0["dealt"] and st["slices"] - st0["slices"] >= 3
+    finally:
+        engine.set_slot_budget(0)
+        engine.set_bp_log(False)

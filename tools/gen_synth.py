@@ -10,9 +10,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import ccsx_amd as cx  # noqa: E402
 
 
-def records(nzmw, L, passes, hole0=0, seed=20201104, movie="synth"):
-    """(name, subread) pairs of the synthetic set, in file order."""
-    for h in range(hole0, hole0 + nzmw):
+def records(nzmw, L, passes, hole0=0, seed=20201104, movie="synth", holes=None):
+    """(name, subread) pairs of the synthetic set, in file order (`holes`: an
+    explicit hole list instead of hole0 .. hole0 + nzmw - 1)."""
+    for h in (range(hole0, hole0 + nzmw) if holes is None else holes):
         if L:
             subs, _ = cx.synth_zmw(seed, h, L, passes)
         else:
@@ -24,9 +25,9 @@ def records(nzmw, L, passes, hole0=0, seed=20201104, movie="synth"):
             qs += len(s)
 
 
-def write(path, nzmw, L, passes, hole0=0, seed=20201104, movie="synth"):
+def write(path, nzmw, L, passes, hole0=0, seed=20201104, movie="synth", holes=None):
     with open(path, "wb") as f:
-        for name, s in records(nzmw, L, passes, hole0, seed, movie):
+        for name, s in records(nzmw, L, passes, hole0, seed, movie, holes):
             f.write(b">%s\n%s\n" % (name, s))
 
 

@@ -12,7 +12,7 @@ for L in "$@"; do
 done
 for i in 1 2 3; do
   for L in "$@"; do
-    CCSX_LIB=$L timeout -k 10 200 python3 bench.py --no-cpu-baseline --e2e-zmws 0 > gpurun_out/$TAG/t_${L}_$i.json 2> gpurun_out/$TAG/t_${L}_$i.err || exit 1
+    CCSX_LIB=$L timeout -k 10 200 python3 bench.py --no-cpu-baseline --e2e-zmws 0 --e-zmws 0 --roofline-zmws 0 > gpurun_out/$TAG/t_${L}_$i.json 2> gpurun_out/$TAG/t_${L}_$i.err || exit 1
     python3 -c "import json; d=json.load(open('gpurun_out/$TAG/t_${L}_$i.json')); print('$L', d['ms_per_step'])"
   done
 done

@@ -31,7 +31,7 @@ export TMPDIR=/tmp
 cd "$R" || exit 1
 
 bench_args() {  # CFG [KCFG]
-  local a="--config $1 --steps 3 --warmup 1 --no-cpu-baseline --e2e-zmws 0"
+  local a="--config $1 --steps 3 --warmup 1 --no-cpu-baseline --e2e-zmws 0 --e-zmws 0 --roofline-zmws 0"
   [ -n "$2" ] && a="$a --kcfg $2"
   echo "$a"
 }
@@ -78,7 +78,7 @@ step() {
         python3 -c "import json,sys; d=json.load(open(sys.argv[1]))['e2e']; print(sys.argv[1], d['value'], 'ZMWs/s', d['s'], 's', d['gcups'], 'GCUPS', 'first', d['first_call_s'])" "$f" ;;
     kt)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_$cfg" -o kt -- \
-        python3 "$R/bench.py" --config "$cfg" --no-cpu-baseline --e2e-zmws 0 > "$OUT/kt_$cfg.json" 2> "$OUT/kt_$cfg.err") &&
+        python3 "$R/bench.py" --config "$cfg" --no-cpu-baseline --e2e-zmws 0 --e-zmws 0 --roofline-zmws 0 > "$OUT/kt_$cfg.json" 2> "$OUT/kt_$cfg.err") &&
         echo "kt $cfg done" ;;
     pmc)
       timeout -k 10 900 bash "$R/tools/pmc_pass.sh" "$TAG/pmc_$cfg" --config "$cfg" > "$OUT/pmc_$cfg.log" 2>&1 && echo "pmc $cfg done" ;;

@@ -49,7 +49,7 @@ durs = [d for _, d in sorted(durs)]
 timed = durs[-int(bench["steps"]):] if durs else []
 timed_ms = sum(timed) / len(timed) / 1e6 if timed else float("nan")
 lines += ["", f"bench.py (same run, {bench['warmup']} warmup + {bench['steps']} timed launches): avg timed launch "
-          f"{bench['roofline']['avg_launch_ms']} ms (HIP events), steps {bench.get('step_ms')}; rocprof avg over all "
+          f"{bench['roofline']['avg_launch_ms']} ms (HIP events), steps {bench.get('step_ms') or bench['roofline'].get('launch_ms')}; rocprof avg over all "
           f"launches {avg_ns / 1e6:.3f} ms (includes the cold first launch); rocprof avg over the "
           f"{len(timed)} timed launches {timed_ms:.3f} ms (kernel trace).", "",
           "## PMC (per launch of ccsx_zmw_kernel, one-launch runs)", "",
@@ -67,8 +67,15 @@ derived = {
     "frac_wait_inst_any": c.get("SQ_WAIT_INST_ANY", 0) / cyc if cyc else None,
     "frac_active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0) / cyc if cyc else None,
     "hbm_fetch_bytes": fetch_b, "hbm_write_bytes": write_b,
-    "effective_clock_GHz": c.get("GRBM_GUI_ACTIVE", 0) / 8 / avg_ns if avg_ns else None,
 }
+# GRBM_GUI_ACTIVE (summed over the 8 XCDs) against the PMC pass's own launch
+# (HIP events of that one-launch run), not the warm timed average
+pmc1 = os.path.join(src, "pmc1_bench.json")
+if os.path.exists(pmc1):
+    pb = json.loads(open(pmc1).read().strip().splitlines()[-1])
+    pmc_ms = pb["roofline"]["avg_launch_ms"]
+    derived["pmc_pass_launch_ms"] = pmc_ms
+    derived["effective_clock_GHz"] = c.get("GRBM_GUI_ACTIVE", 0) / 8 / (pmc_ms * 1e6) if pmc_ms else None
 lines += ["", "## Derived", "", "| quantity | value |", "|---|---|"]
 for n, v in derived.items():
     lines.append(f"| {n} | {v if v is None else (round(v, 4) if isinstance(v, float) else v)} |")
