@@ -55,7 +55,7 @@ struct opoa_s {
     /* results */
     uint32_t ncns, ncols, ccap;
     uint8_t *cns, *ccons;
-    uint32_t *msaidxs, msacap;
+    uint32_t *msaidxs, msacap, idxcap;  /* msacols bytes, msaidxs entries */
     uint8_t *msacols;
     uint32_t mrow;
     uint64_t cells;
@@ -534,7 +534,12 @@ void opoa_tidy_msa(opoa_t *g)
     if ((size_t)nc * mrow + 1 > g->msacap) {
         g->msacap = (uint32_t)((size_t)nc * mrow * 2 + 16);
         g->msacols = xrealloc(g->msacols, g->msacap);
-        g->msaidxs = xrealloc(g->msaidxs, (size_t)g->msacap * 4 / (mrow ? mrow : 1) + 16);
+    }
+    /* its own capacity: a later POA with fewer reads (smaller mrow) can have
+     * more columns in the same msacols bytes */
+    if (nc + 1 > g->idxcap) {
+        g->idxcap = nc * 2 + 16;
+        g->msaidxs = xrealloc(g->msaidxs, (size_t)g->idxcap * 4);
     }
     memset(g->msacols, 4, (size_t)nc * mrow);
     uint32_t col = 0;

@@ -123,3 +123,20 @@ def test_edit_identity_known_answers():
                 b.insert(k, rnd.choice(b"ACGT"))
         assert abs(edit_identity(a, bytes(b)) - _edit_identity(a, bytes(b))) < 1e-12
     assert edit_identity(b"", b"ACGT") == 0.0
+
+
+def test_oracle_object_reuse_fewer_reads_more_columns():
+    """One POA object (a batch thread's) runs a config-E ZMW, then a 2-pass
+    ZMW whose MSA has fewer rows but more columns: the MSA index array has its
+    own capacity (it was sized from the byte capacity and the old row count,
+    and the second ZMW wrote past it)."""
+    import bench
+    import ccsx_amd as cx
+    from oracle.oracle import batch
+    from tests.zmw_cases import synth
+    h = 10_500_000
+    big = cx.prepare(cx.synth_zmw(bench.SEED, h, *bench.zmw_shape(bench.CONFIGS["E"], h))[0])
+    small = synth(7502, 9000, 2)
+    both, _, _ = batch([big, small], 0, 1)
+    alone, _, _ = batch([small], 0, 1)
+    assert both[1] == alone[0] and len(alone[0]) > 9000
