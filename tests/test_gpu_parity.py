@@ -353,7 +353,7 @@ def test_multi_slice_run(engine):
         assert st["dealt"] - st0["dealt"] >= 1
         assert st["parts"] - st0["parts"] >= 4
         assert st["reruns"] - st0["reruns"] >= 2
-        assert st["slices"] - st0["slices"] >= 6  # >= 4 parts + the re-run
+        assert st["slices"] - st0["slices"] >= 5  # >= 4 parts + the re-run
         ref = Poa()
         for i in (0, 20, 21, 70, 71, len(zs) - 1):
             _, bps = ref.zmw_breakpoints(zs[i].seqs, zs[i].offs, zs[i].lens)

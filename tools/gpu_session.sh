@@ -11,6 +11,7 @@
 #   bench:CFG[:KCFG]   bench.py --config CFG (B|C|D|E|H), 3 steps, optional forced kernel cfg
 #   benchn:CFG:N[:KCFG] the same with N ZMWs per GPU
 #   ab:CFG:KCFG,...[:LIB,...]  3 interleaved rounds of bench --config CFG over kernel cfgs x libraries
+#   abx:LINE:LIB,...   3 interleaved rounds of bench lines (B|C|D|E16k) over libraries
 #   e2e:N[:KCFG]       bench.py's end-to-end line (config E, ccsx_gpu_run) on N ZMWs per GPU
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
@@ -69,6 +70,17 @@ step() {
             CCSX_LIB=$L timeout -k 10 600 python -u bench.py $(bench_args "$cfg" "$kk") > "$f" 2> "${f%.json}.err" || return 1
             python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'k', sys.argv[3], d['ms_per_step'], 'ms', d['gcups'], 'GCUPS')" "$f" "$L" "$kk"
           done
+        done
+      done ;;
+    abx)  # abx:LINE:LIB,LIB... -- 3 interleaved rounds, LINE = B | D | C | E16k (16,384 config-E ZMWs per launch)
+      local i f L a
+      if [ "$cfg" = E16k ]; then a="--no-kernel-line --roofline-zmws 16384 --steps 3 --warmup 1 --no-cpu-baseline --e2e-zmws 0 --e-zmws 0"
+      else a="$(bench_args "$cfg")"; fi
+      for i in 1 2 3; do
+        for L in ${k//,/ }; do
+          f="$OUT/abx_${cfg}_${L%.so}_$i.json"
+          CCSX_LIB=$L timeout -k 10 600 python -u bench.py $a > "$f" 2> "${f%.json}.err" || return 1
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], d['ms_per_step'], 'ms', d['gcups'], 'GCUPS', d['roofline']['avg_launch_ms'])" "$f" "$L" "$cfg"
         done
       done ;;
     e2e)  # e2e:N[:KCFG] -- bench.py's config-E end-to-end line on N ZMWs (CCSX_KCFG forces a kernel cfg)
