@@ -18,6 +18,8 @@
 // ZMWs of the run are written (the reference has no per-ZMW failure).
 #include <errno.h>
 #include <getopt.h>
+#include <malloc.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -40,9 +42,55 @@
 
 namespace {
 
+// Bases of a chunk's ZMWs live in one arena per chunk (an anonymous mapping
+// with transparent huge pages), recycled through a pool: per-ZMW strings
+// (~130 KB each, ~2 GB per 16,384-ZMW chunk) cost a page fault per 4 KB page
+// when written and a page-table teardown when freed -- 0.55 s per chunk at
+// the process exit, which the CLI's timed run pays for every chunk still held.
+class ArenaPool {
+public:
+    struct Arena {
+        char *p = nullptr;
+        size_t cap = 0;
+    };
+    Arena get(size_t need)
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            for (size_t i = 0; i < free_.size(); ++i)
+                if (free_[i].cap >= need) {
+                    Arena a = free_[i];
+                    free_.erase(free_.begin() + (long)i);
+                    return a;
+                }
+        }
+        Arena a;
+        a.cap = std::max<size_t>((need + need / 8 + (2u << 20) - 1) & ~size_t((2u << 20) - 1), 2u << 20);
+        void *p = mmap(nullptr, a.cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) {
+            fprintf(stderr, "[ccsx] cannot map %zu bytes for a chunk's bases\n", a.cap);
+            std::_Exit(1);
+        }
+        if (!getenv("CCSX_NO_THP")) (void)madvise(p, a.cap, MADV_HUGEPAGE);
+        a.p = static_cast<char *>(p);
+        return a;
+    }
+    void put(Arena a)
+    {
+        if (!a.p) return;
+        std::lock_guard<std::mutex> g(m_);
+        free_.push_back(a);
+    }
+
+private:
+    std::mutex m_;
+    std::vector<Arena> free_;
+};
+
 struct Zmw {
     ccsx_ingest::ZmwRef ref;  // the subreads as spans of the input blocks (until assembled)
-    std::string movie, hole, seqs;
+    std::string movie, hole;
+    char *seqs = nullptr;     // the bases (in the chunk's arena)
     std::vector<uint32_t> lens;
     std::vector<uint32_t> seg_off, seg_len;
     std::vector<uint8_t> seg_rev;
@@ -54,6 +102,12 @@ struct Zmw {
 struct Chunk {
     size_t id = 0;
     std::vector<Zmw> zs;
+    ArenaPool *pool = nullptr;
+    ArenaPool::Arena arena;  // the ZMWs' bases
+    ~Chunk()
+    {
+        if (pool) pool->put(arena);
+    }
     std::atomic<size_t> pending{0};  // batches not yet back from a device
     double t_read0 = 0, t_read1 = 0;  // CCSX_TIMING: when step 0's reader read it
 };
@@ -88,7 +142,7 @@ int usage()
             "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
             "CCSX_CHUNK     Largest chunk in ZMWs [8192 x contexts]\n"
-            "CCSX_CHUNK0    First chunk in ZMWs [1024], growing x4 up to CCSX_CHUNK\n"
+            "CCSX_CHUNK0    First chunk in ZMWs [CCSX_CHUNK / 2], growing x4 up to CCSX_CHUNK\n"
             "CCSX_KCFG      Force a kernel configuration (0 latency, 1 occupancy, 2 throughput, 3 solo)\n"
             "CCSX_DEV_SHARE Processes sharing each GPU [1] (each context's memory share shrinks)\n"
             "\n"
@@ -103,8 +157,13 @@ int usage()
 // input blocks (the copy step 0 of the reference makes, main.c:674-685), then
 // ccs_prepare + strand flip (the CPU half of step 1, main.c:520-536, with its
 // -v output)
-void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
+void prepare_chunk(Chunk &ch, int nthreads, int verbose)
 {
+    std::vector<Zmw> &zs = ch.zs;
+    // each ZMW's bases at its offset in the chunk's arena
+    std::vector<size_t> at(zs.size() + 1, 0);
+    for (size_t i = 0; i < zs.size(); ++i) at[i + 1] = at[i] + zs[i].ref.total();
+    ch.arena = ch.pool->get(at.back());
     std::atomic<size_t> next(0);
     auto work = [&]() {
         std::string msg;
@@ -112,7 +171,7 @@ void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
             Zmw &z = zs[i];
             z.movie = std::move(z.ref.movie);
             z.hole = std::move(z.ref.hole);
-            z.seqs.resize(z.ref.total());
+            z.seqs = ch.arena.p + at[i];
             z.lens.resize(z.ref.recs.size());
             size_t o = 0;
             for (size_t k = 0; k < z.ref.recs.size(); ++k) {
@@ -127,7 +186,7 @@ void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
             z.seg_off.resize(n);
             z.seg_len.resize(n);
             z.seg_rev.resize(n);
-            const uint32_t ns = ccsx_prepare(&z.seqs[0], z.lens.data(), n, z.seg_off.data(), z.seg_len.data(),
+            const uint32_t ns = ccsx_prepare(z.seqs, z.lens.data(), n, z.seg_off.data(), z.seg_len.data(),
                                              z.seg_rev.data());
             z.seg_off.resize(ns);
             z.seg_len.resize(ns);
@@ -142,7 +201,7 @@ void prepare_chunk(std::vector<Zmw> &zs, int nthreads, int verbose)
                     snprintf(h, sizeof h, ">%s_%u/%u strand=%d len=%u \n", z.hole.c_str(), l, ns, z.seg_rev[l],
                              z.seg_len[l]);
                     msg += h;
-                    msg.append(z.seqs, z.seg_off[l], z.seg_len[l]);
+                    msg.append(z.seqs + z.seg_off[l], z.seg_len[l]);
                     msg += '\n';
                 }
             }
@@ -327,6 +386,15 @@ std::unordered_set<std::string> exclude_holes(std::string &buf, const char *arg)
 int main(int argc, char **argv)
 {
     const auto tmain = std::chrono::steady_clock::now();
+    // per-ZMW strings (~130 KB of subreads each, a few GB per chunk) from the
+    // heap, not one mmap each: freed memory is reused by the next chunk with
+    // no munmap / page-fault churn, and nothing is returned to the kernel
+    // mid-run (freeing a 16,384-ZMW chunk of mmap'd strings took 0.7 s, and
+    // the process exit paid the same for the chunks still held)
+    if (!getenv("CCSX_MALLOC_DEFAULT")) {
+        mallopt(M_MMAP_THRESHOLD, 32 << 20);
+        mallopt(M_TRIM_THRESHOLD, 1 << 30);
+    }
     int c, verbose = 0, min_subread_len = 5000, max_subread_len = 500000, min_fulllen_count = 3, nthreads = 1;
     int isbam = 1, split_subread = 1;
     std::unordered_set<std::string> hole_set;
@@ -423,13 +491,16 @@ int main(int argc, char **argv)
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     const auto tstart = std::chrono::steady_clock::now();
     if (timing)
-        fprintf(stderr, "[ccsx] %d device context(s) open at %.0f ms after main\n", nctx,
-                std::chrono::duration<double, std::milli>(tstart - tmain).count());
+        fprintf(stderr, "[ccsx] %d device context(s) open at %.0f ms after main (main at epoch %.3f s)\n", nctx,
+                std::chrono::duration<double, std::milli>(tstart - tmain).count(),
+                std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count() -
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - tmain).count());
     auto now_ms = [tstart]() {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tstart).count();
     };
     const int mode = split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE;
 
+    ArenaPool arenas;  // (declared before every holder of a chunk)
     BatchQueue queue;
     ChunkRing ring(3);
     std::atomic<bool> fatal(false);
@@ -451,7 +522,7 @@ int main(int argc, char **argv)
                 out.assign(b.idx.size(), ccsx_zmw_out{});
                 for (size_t i = 0; i < b.idx.size(); ++i) {
                     const Zmw &z = ch.zs[b.idx[i]];
-                    in[i] = ccsx_zmw_in{z.seqs.data(), z.seg_off.data(), z.seg_len.data(), (uint32_t)z.seg_len.size()};
+                    in[i] = ccsx_zmw_in{z.seqs, z.seg_off.data(), z.seg_len.data(), (uint32_t)z.seg_len.size()};
                     if (!fault_hole.empty() && z.hole == fault_hole) ccsx_gpu_set_fault(ctx[w], (int64_t)i);
                 }
                 const double t0 = now_ms();
@@ -539,15 +610,20 @@ int main(int argc, char **argv)
     // step 0's reading on its own thread, one chunk ahead of the preparation
     // (the reference's step 0 does both in turn: main.c:652-697)
     ReadQueue rq(1);
-    // first chunk: the reference's 1,024 (CCSX_CHUNK0 overrides; the chunk
-    // sizes change only how the work is cut, never the output)
-    size_t chunk0 = 1024;
+    // first chunk: half the largest (the reference starts at 1,024 ZMWs,
+    // main.c:686-690, which here only fed small launches on the latency /
+    // occupancy objects while the device idled: 62,500 config-E ZMWs 6.3 s
+    // with 1,024, 5.4 s with 8,192, 5.8 s with 16,384, r04e; CCSX_CHUNK0
+    // overrides -- the chunk sizes change only how the work is cut, never
+    // the output)
+    size_t chunk0 = std::max<size_t>(1024, chunk_max / 2);
     if (const char *e = getenv("CCSX_CHUNK0")) chunk0 = std::max<size_t>(1, std::min<size_t>(chunk_max, strtoull(e, nullptr, 10)));
     std::thread reader([&]() {
         size_t chunk_size = chunk0;
         for (size_t id = 0;; ++id) {
             auto ch = std::make_shared<Chunk>();
             ch->id = id;
+            ch->pool = &arenas;
             std::vector<Zmw> &zs = ch->zs;
             ch->t_read0 = now_ms();
             ccsx_ingest::ZmwRef zr;
@@ -579,7 +655,7 @@ int main(int argc, char **argv)
         std::vector<Zmw> &zs = ch->zs;
         const size_t id = ch->id;
         const double t0 = ch->t_read0, t1 = ch->t_read1;
-        prepare_chunk(zs, nthreads, verbose);
+        prepare_chunk(*ch, nthreads, verbose);
         // cost-balanced micro-batches: cost ranks dealt round-robin, each
         // batch longest first (dispatch.cpp)
         const uint32_t n = (uint32_t)zs.size();
@@ -619,9 +695,20 @@ int main(int argc, char **argv)
         bool werr = fp_out != stdout && (ferror(fp_out) || fclose(fp_out) != 0);
         werr = (ferror(stdout) || fflush(stdout) != 0) || werr;  // (-v >= 3 breakpoint lines go to stdout)
         if (werr) fprintf(stderr, "[ccsx] error writing the output: %s\n", strerror(errno));
+        if (getenv("CCSX_EXIT_CLOSE")) {  // measurement: the teardown steps the exit skips, timed
+            const double a = now_ms();
+            for (auto *x : ctx) ccsx_gpu_close(x);
+            const double b = now_ms();
+            rd.reset();
+            const double d = now_ms();
+            last_written.reset();
+            fprintf(stderr, "[ccsx] teardown: contexts %.0f ms, input %.0f ms, last chunk %.0f ms\n", b - a, d - b,
+                    now_ms() - d);
+        }
         if (timing)
-            fprintf(stderr, "[ccsx] output done at %.0f ms; device cells %llu\n", tw,
-                    (unsigned long long)cells_total.load());
+            fprintf(stderr, "[ccsx] output done at %.0f ms; device cells %llu; exit at epoch %.3f s\n", tw,
+                    (unsigned long long)cells_total.load(),
+                    std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count());
         if (nfail) fprintf(stderr, "[ccsx] %zu ZMWs had no CCS (device status, see above)\n", nfail);
         fflush(stderr);
         std::_Exit(werr ? 1 : 0);

@@ -49,13 +49,24 @@ def main():
                         env[k] = x
                 tag = v.replace(",", "_").replace("=", "")
                 with open(fa, "rb") as f, open(os.path.join(a.out, f"{tag}_{r}.log"), "w") as log:
+                    e0 = time.time()
                     t0 = time.perf_counter()
                     p = subprocess.run([BIN, "-A", "-j", str(a.jobs), "-", "/dev/null"], stdin=f, stderr=log, env=env)
                     dt = time.perf_counter() - t0
+                    e1 = time.time()
                 if p.returncode != 0:
                     raise SystemExit(f"variant {v}: ccsx exited {p.returncode}")
                 res["runs"].setdefault(v, []).append(round(dt, 3))
-                print(f"{v}: {dt:.2f} s = {a.n / dt:.0f} ZMWs/s", flush=True)
+                # before main / after the CLI's last line (process start, exit)
+                pre = post = None
+                for line in open(os.path.join(a.out, f"{tag}_{r}.log")):
+                    if "main at epoch" in line:
+                        pre = float(line.split("main at epoch ")[1].split()[0]) - e0
+                    if "exit at epoch" in line:
+                        post = e1 - float(line.split("exit at epoch ")[1].split()[0])
+                res.setdefault("pre_main_s", {}).setdefault(v, []).append(pre)
+                res.setdefault("exit_s", {}).setdefault(v, []).append(post)
+                print(f"{v}: {dt:.2f} s = {a.n / dt:.0f} ZMWs/s (before main {pre}, exit {post})", flush=True)
     finally:
         if os.path.exists(fa):
             os.remove(fa)
