@@ -246,8 +246,8 @@ def cli_child_env(local: int, ndev: int, sharing: int) -> dict:
 def cli_cells(log_path: str) -> int:
     with open(log_path) as f:
         for line in f:
-            if "device cells" in line:
-                return int(line.rsplit(" ", 1)[1])
+            if "device cells " in line:
+                return int(line.split("device cells ")[1].split(";")[0].split()[0])
     return 0
 
 
