@@ -476,6 +476,7 @@ def main():
     ap.add_argument("--no-kernel-line", action="store_true", help="skip the --config kernel line (profiling runs)")
     ap.add_argument("--kcfg", type=int, default=-1, help="force a kernel configuration (0 latency, 1 occupancy, 3 solo, "
                                                          "2 throughput; -1: by slice size)")
+    ap.add_argument("--wg-cap", type=int, default=0, help="measurement: at most this many workgroups per CU (0: off)")
     ap.add_argument("--out-dir", default=os.path.join(ROOT, "gpurun_out", "bench"), help="CLI logs")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
@@ -507,7 +508,11 @@ def main():
         eng.set_mem_share(sharing)
     if args.kcfg >= 0:
         eng.set_kernel_cfg(args.kcfg)
+    if args.wg_cap:
+        eng.set_wg_cap(args.wg_cap)
     overrides = {k: os.environ[k] for k in ("CCSX_LIB",) if os.environ.get(k)}
+    if args.wg_cap:
+        overrides["wg_cap"] = args.wg_cap
     threads, _, _ = cpu_share()
 
     # config B (or --config): K launches, inputs resident

@@ -83,6 +83,15 @@ step() {
           python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], d['ms_per_step'], 'ms', d['gcups'], 'GCUPS', d['roofline']['avg_launch_ms'])" "$f" "$L" "$cfg"
         done
       done ;;
+    wgcap)  # wgcap:LINE:CAP,CAP... -- the residency curve of a bench line (B|D|E16k) by workgroups per CU
+      local i f c a
+      if [ "$cfg" = E16k ]; then a="--no-kernel-line --roofline-zmws 16384 --steps 3 --warmup 1 --no-cpu-baseline --e2e-zmws 0 --e-zmws 0"
+      else a="$(bench_args "$cfg")"; fi
+      for c in ${k//,/ }; do
+        f="$OUT/wgcap_${cfg}_w$c.json"
+        timeout -k 10 600 python -u bench.py $a --wg-cap "$c" > "$f" 2> "${f%.json}.err" || return 1
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'wg', sys.argv[3], d['ms_per_step'], 'ms', d['gcups'], 'GCUPS')" "$f" "$cfg" "$c"
+      done ;;
     e2e)  # e2e:N[:KCFG] -- bench.py's config-E end-to-end line on N ZMWs (CCSX_KCFG forces a kernel cfg)
       local f="$OUT/e2e_${cfg}${k:+_k$k}${CCSX_SHRED_READ_CAP:+_rc$CCSX_SHRED_READ_CAP}.json"
       CCSX_KCFG=${k:--1} CCSX_TIMING=1 timeout -k 10 600 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline \
