@@ -332,7 +332,7 @@ const char *ccsx_gpu_status_str(int32_t s)
 constexpr size_t kPinnedSeqFloor = 512ull << 20, kPinnedOutFloor = 128ull << 20;
 
 // LDS read buffer limits of the LDS kernel instance: reads up to 100 kb
-// (50 KiB of nibble pairs, 2 workgroups per CU) and 4,096 segments; beyond
+// (25 KiB of 2-bit codes) and 4,096 segments; beyond
 // them a slice runs the HBM-read instance
 constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
 // slices of at least this many times the occupancy configuration's resident
@@ -427,7 +427,7 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
     s.seq_bytes = seq_b, s.ws_bytes = ws_b, s.out_bytes = out_b, s.msa_bytes = msa_b;
     s.bp_words = bp_w;
     s.nseg_total = nseg;
-    // nibble-pair read buffer (ccsx_kernel.hip load_read); at least one band:
+    // 2-bit read buffer (ccsx_kernel.hip stage_read); at least one band:
     // every lane reads its window bytes even when the read is shorter.  A
     // slice with a read or a cursor array beyond the LDS budget runs the
     // HBM-read kernel instance (lds_read_words = 0)
@@ -443,7 +443,7 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
         // one more workgroup per CU
         uint32_t lb = std::max<uint32_t>(lmax_all, ccsx::kW);
         if (shred_tight) lb = std::min(lb, c->shred_read_cap);
-        s.lds_read_words = (lb + 7) / 8 + 2;
+        s.lds_read_words = (lb + 15) / 16 + 2;
         s.lds_nmax = std::max<uint32_t>(nmax, 1);
     }
     // LDS words after the configuration's fixed part: the read buffer and

@@ -174,7 +174,7 @@ struct Z {
     uint8_t *ws;
     const uint8_t *seq;
     int32_t *lds;        // workgroup LDS: DP ring (kRingA rows x kRowW words), offsets, job, read
-    uint8_t *rd;         // read as nibble pairs: byte b = pair(2b) | pair(2b+1) << 4, pair(j) = code(j) | code(j+1) << 2
+    uint8_t *rd;         // read as 2-bit codes: byte b = code(4b) | code(4b+1) << 2 | code(4b+2) << 4 | code(4b+3) << 6
     // HBM-read instance: an LDS window of the read (rd_window), two chunks of
     // kWinChunk bases resident, the first one wa (wave 0's view)
     uint8_t *win;
@@ -258,7 +258,7 @@ __device__ __forceinline__ uint64_t *G_mem(const Z &z, int b) { return P<uint64_
 __device__ __forceinline__ uint32_t *G_poff(const Z &z, int b) { return P<uint32_t>(z, b ? z.L.poff1 : z.L.poff0); }
 __device__ __forceinline__ uint32_t *G_pred(const Z &z, int b) { return P<uint32_t>(z, b ? z.L.pred1 : z.L.pred0); }
 
-__device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return ((uint32_t)z.rd[j >> 1] >> ((j & 1u) * 4u)) & 3u; }
+__device__ __forceinline__ uint32_t rcode(const Z &z, uint32_t j) { return ((uint32_t)z.rd[j >> 2] >> ((j & 3u) * 2u)) & 3u; }
 
 // ----------------------------------------------------------------------------
 // The HBM-read instance's read window.  Reads beyond the LDS read buffer live
@@ -279,50 +279,59 @@ __device__ __forceinline__ void win_load(const Z &z, uint32_t c)
     const uint32_t lane = lane_id();
     const auto rs = brsrc(z.rd, z.rdbytes);  // beyond the buffer: zeros
 #pragma unroll
-    for (uint32_t k = 0; k < kWinChunk / 2 / 1024; ++k) {
-        const uint32_t b = c * (kWinChunk / 2) + k * 1024 + lane * 16;
+    for (uint32_t k = 0; k < kWinChunk / 4 / 1024; ++k) {
+        const uint32_t b = c * (kWinChunk / 4) + k * 1024 + lane * 16;
         const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, b, 0, 0);
         *reinterpret_cast<v4u *>(z.win + (b & kWinBytesMask)) = v;
     }
     wsync();
 }
 
-// bases [off, off + 132) within chunks [c0, c0 + nc) (uniform)
+// bases [off, off + 136) within chunks [c0, c0 + nc) (uniform): every byte
+// a row's rd_win16 reads
 __device__ __forceinline__ bool win_has(uint32_t c0, uint32_t nc, int32_t off)
 {
-    return (uint32_t)off >= c0 * kWinChunk && (uint32_t)off + 132u <= (c0 + nc) * kWinChunk;
+    return (uint32_t)off >= c0 * kWinChunk && (uint32_t)off + 136u <= (c0 + nc) * kWinChunk;
 }
 
-// lane's byte (off >> 1) + lane + d of the read (the LDS buffer, or the
-// window / HBM on the HBM-read instance; `inwin`: the wave may trust the
-// window for this row)
-__device__ __forceinline__ uint32_t rd_byte(const Z &z, int32_t off, uint32_t d, bool inwin)
+// lane's 16-bit window of the read for a row at band offset `off`: the codes
+// of positions P .. P + 7, P = (off + 2 lane) & ~3 -- bytes (off + 2 lane) >> 2
+// and the next, from the LDS buffer, or the window / HBM on the HBM-read
+// instance (`inwin`: the wave may trust the window for this row).  The
+// lane's cells t = 2 lane, 2 lane + 1 of a row at offset off + d (0 <= d <= 3)
+// are win_codes(window, off, d).
+__device__ __forceinline__ uint32_t rd_win16(const Z &z, int32_t off, bool inwin)
 {
-    const uint32_t b = (uint32_t)(off >> 1) + lane_id() + d;
-    if (!z.hbm) return z.rd[b];
-    return inwin ? z.win[b & kWinBytesMask] : z.rd[b];
+    const uint32_t b = ((uint32_t)off + 2u * lane_id()) >> 2;
+    if (!z.hbm) return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
+    if (inwin) return (uint32_t)z.win[b & kWinBytesMask] | (uint32_t)z.win[(b + 1) & kWinBytesMask] << 8;
+    return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
+}
+
+// the codes of read positions off + d + 2 lane (bits 0-1) and the next (bits
+// 2-3) from the window rd_win16(z, off) loaded
+__device__ __forceinline__ uint32_t win_codes(uint32_t win, int32_t off, int32_t d)
+{
+    return win >> ((((uint32_t)off + 2u * lane_id()) & 3u) * 2u + 2u * (uint32_t)d);
 }
 
 // ----------------------------------------------------------------------------
-// push: stage read k (ASCII in HBM) into LDS as nibble pairs: the byte at
-// (off >> 1) + l holds, in nibble off & 1, the codes of read positions
-// off + 2l and off + 2l + 1 -- one ds_read_u8 per lane per DP row
+// push: stage read k (ASCII in HBM) into LDS as 2-bit codes, four per byte
+// (word w = positions 16 w .. 16 w + 15): 4,096 bases in 1 KiB, so the solo
+// object's workgroup fits 16 per CU; a DP row reads two bytes per lane
+// (rd_win16)
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void stage_read(const Z &z, const uint8_t *src, uint32_t m, uint32_t tid, uint32_t T)
 {
-    const uint32_t nwd = (m + 7) / 8 + 1;
+    const uint32_t nwd = (m + 15) / 16 + 1;
     uint32_t *dst = reinterpret_cast<uint32_t *>(z.rd);
     for (uint32_t w = tid; w < nwd; w += T) {
-        uint32_t c[9];
-#pragma unroll
-        for (uint32_t b = 0; b < 9; ++b) {
-            const uint32_t j = w * 8 + b;
-            c[b] = j < m ? enc_base(src[j]) : 0u;
-        }
         uint32_t x = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-            x |= (c[2 * k] | c[2 * k + 1] << 2 | c[2 * k + 1] << 4 | c[2 * k + 2] << 6) << (8 * k);
+        for (uint32_t b = 0; b < 16; ++b) {
+            const uint32_t j = w * 16 + b;
+            x |= (j < m ? enc_base(src[j]) : 0u) << (2 * b);
+        }
         dst[w] = x;
     }
 }
@@ -664,7 +673,7 @@ struct AState {
     int32_t H0, H1, D0, D1;  // row r-1, this lane's two cells
     int32_t pOff, pArg;      // row r-1: band offset, position of its maximum
     int32_t vOff, vKey;      // lane (q & 63): band offset / row-max key of row q
-    uint32_t qn;             // read codes at the next row's chain offset (loaded a row ahead)
+    uint32_t qn;             // rd_win16 at this row's offset pOff: the next row's read codes (loaded a row ahead)
     uint32_t nspill;         // spill records written
     uint64_t fmask;          // bit q & 63: row q is a chain row without far / spill flags
     uint32_t ring;           // LDS word offset of this row's ring slot ((r % kRingA) * kRowW)
@@ -779,7 +788,6 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t base = info & 3u;
     const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
-    const int32_t pb = S.pOff & ~1;  // S.qn: read bytes (pOff >> 1) + lane, + 1
     const int32_t sh = coff - S.pOff;
     // (an integer test keeps the branch scalar: a bool of && lowers to a lane mask)
     const uint32_t fast = (uint32_t)(S.fmask >> li) & ((uint32_t)sh <= 1u ? 1u : 0u);
@@ -794,10 +802,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
                     bool cold) __attribute__((always_inline)) {
         // the next row's read window, a row ahead of its use (its offset lies
         // in [off, off + 3] on every fast row)
-        {
-            const bool w = z.hbm && win_has(z.wa, 2, off);
-            S.qn = rd_byte(z, off, 0, w) | rd_byte(z, off, 1, w) << 8;
-        }
+        S.qn = rd_win16(z, off, z.hbm && win_has(z.wa, 2, off));
         const uint32_t q0 = qp & 3u, q1 = (qp >> 2) & 3u;
         const int32_t srcu = c.src0 + kE * off;
         // (the fast rows fold the j = 0 leading term into Mh0, see below)
@@ -882,7 +887,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         // row at offset 0 (band unmoved) is the read-prefix source 0 instead
         // of -inf (SPEC.md §3.2 src(0) = 0): it rides in as the DPP's old
         // value, max(0, src) = 0, so the tail needs no lane test.
-        const uint32_t qp = S.qn >> (4u * (uint32_t)(coff - pb));  // coff - pb in [0, 2]
+        const uint32_t qp = win_codes(S.qn, S.pOff, sh);  // sh in [0, 1]
         // band move 0 or 1 as a scalar branch: each side shifts only what it
         // needs (no selects)
         if (sh == 0) {
@@ -907,9 +912,9 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         ckind = kind;
 #endif
         (void)kind;
-        const uint32_t d = (uint32_t)(off - pb);
-        const uint32_t qp =
-            d <= 3u ? S.qn >> (4u * d) : rd_byte(z, off, 0, z.hbm && win_has(z.wa, 2, off)) >> ((uint32_t)(off & 1) * 4u);
+        const uint32_t d = (uint32_t)(off - S.pOff);
+        const uint32_t qp = d <= 3u ? win_codes(S.qn, S.pOff, (int32_t)d)
+                                    : win_codes(rd_win16(z, off, z.hbm && win_has(z.wa, 2, off)), off, 0);
         tail(off, qp, Mh0, Mh1, Dv0, Dv1, true);
     }
 }
@@ -1073,7 +1078,7 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t np = info >> 8;
     const int32_t off = __builtin_amdgcn_readlane(vOff, li);
-    const uint32_t qp = rd_byte(z, off, 0, z.hbm && win_has(S.wc0, S.wnc, off)) >> ((uint32_t)(off & 1) * 4u);
+    const uint32_t qp = win_codes(rd_win16(z, off, z.hbm && win_has(S.wc0, S.wnc, off)), off, 0);
     const int2 Dv = reinterpret_cast<const int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kDc + c.L2)[0];
     PredAcc A;
     A.Dv0 = Dv.x, A.Dv1 = Dv.y;
@@ -1149,7 +1154,7 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
     AState S;
     S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
     S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
-    S.qn = rd_byte(z, 0, 0, true) | rd_byte(z, 0, 1, true) << 8;
+    S.qn = rd_win16(z, 0, true);
     S.nspill = 0;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
@@ -1269,7 +1274,6 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
     const uint32_t base = info & 3u;
     const uint32_t np = info >> 8;
     const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
-    const int32_t pb = S.pOff & ~1;  // S.qn: read bytes (pOff >> 1) + lane, + 1
     const int32_t sh = coff - S.pOff;
     const uint32_t fast = (uint32_t)(S.fmask >> li) & ((uint32_t)sh <= 1u ? 1u : 0u);
     // everything after the predecessor terms: the recurrence (dpA_row's
@@ -1278,10 +1282,7 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
     // tags are constants and it meets no further branch
     auto tail = [&](int32_t off, uint32_t qp, const PredAcc &A, bool cold) __attribute__((always_inline)) {
         // the next row's read window, a row ahead of its use
-        {
-            const bool w = z.hbm && win_has(z.wa, 2, off);
-            S.qn = rd_byte(z, off, 0, w) | rd_byte(z, off, 1, w) << 8;
-        }
+        S.qn = rd_win16(z, off, z.hbm && win_has(z.wa, 2, off));
         const int32_t srcu = c.src0 + kE * off;
         const int32_t src0 = (off == 0 && lane == 0) ? 0 : srcu;
         const bool mp0 = A.Mh0 >= src0, mp1 = A.Mh1 >= srcu + kE;
@@ -1348,16 +1349,16 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         }
         A.Dv0 = max(a0, b0), A.Dv1 = max(a1, b1);
         A.dx0 = b0 > a0 ? 4u : 0u, A.dx1 = b1 > a1 ? 4u : 0u;
-        tail(coff, S.qn >> (4u * (uint32_t)(coff - pb)), A, false);
+        tail(coff, win_codes(S.qn, S.pOff, sh), A, false);
     } else {
         PredAcc A;
         int32_t off;
         int kind;
         dpA_cold<true>(z, S, r, info, coff, lim, off, A, kind);
         (void)kind;
-        const uint32_t d = (uint32_t)(off - pb);
-        const uint32_t qp =
-            d <= 3u ? S.qn >> (4u * d) : rd_byte(z, off, 0, z.hbm && win_has(z.wa, 2, off)) >> ((uint32_t)(off & 1) * 4u);
+        const uint32_t d = (uint32_t)(off - S.pOff);
+        const uint32_t qp = d <= 3u ? win_codes(S.qn, S.pOff, (int32_t)d)
+                                    : win_codes(rd_win16(z, off, z.hbm && win_has(z.wa, 2, off)), off, 0);
         tail(off, qp, A, true);
     }
 }
@@ -1411,7 +1412,7 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     AState S;
     S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
     S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
-    S.qn = rd_byte(z, 0, 0, true) | rd_byte(z, 0, 1, true) << 8;
+    S.qn = rd_win16(z, 0, true);
     S.nspill = 0;
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
@@ -2640,7 +2641,7 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
     } else {
         z.rd = reinterpret_cast<uint8_t *>(smem + kLdsFixed);
         z.pos = reinterpret_cast<uint32_t *>(smem + kLdsFixed) + a.lds_read_words;
-        z.rdcap = (a.lds_read_words - 2) * 8;
+        z.rdcap = (a.lds_read_words - 2) * 16;
     }
     z.status = kOk;
     z.cells = 0;

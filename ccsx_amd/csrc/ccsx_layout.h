@@ -34,9 +34,9 @@ constexpr int kRowW = 272;     // LDS words per ring row of the two-wave DP: H a
 constexpr int kRingA = CCSX_RINGA;
 constexpr int kNeg = -(1 << 29);
 // the HBM-read kernel instance's LDS window of the read: two chunks of
-// kWinChunk bases as nibble pairs (ccsx_kernel.hip win_load)
+// kWinChunk bases as 2-bit codes (ccsx_kernel.hip win_load)
 constexpr uint32_t kWinChunk = 8192;
-constexpr uint32_t kRdWinBytes = kWinChunk;
+constexpr uint32_t kRdWinBytes = kWinChunk / 2;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // The kernel configurations (ccsx_kernel.hip is compiled once per
@@ -110,14 +110,14 @@ CCSX_HD inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255)
 //    row (per cell the M and D predecessor slots, u16 each: 512 B per row),
 //    written for rows above 63 predecessors only;
 //  * the HBM-read kernel instance (reads beyond the LDS read buffer): the read
-//    as nibble pairs and the shredding cursors.
+//    as 2-bit codes and the shredding cursors.
 enum ZExt { kExtWtag = 0, kExtRdbuf, kExtPos, kExtEnd };
 
 CCSX_HD inline uint64_t zext_size(const ZmwDesc &d, int which)
 {
     switch (which) {
     case kExtWtag: return uint64_t(d.wcap) * kW * 4;
-    case kExtRdbuf: return uint64_t((d.lcap + 7) / 8 + 2) * 4;
+    case kExtRdbuf: return uint64_t((d.lcap + 15) / 16 + 2) * 4;
     default: return uint64_t(d.n) * 4;
     }
 }
