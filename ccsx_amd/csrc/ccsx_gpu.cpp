@@ -228,6 +228,7 @@ struct ccsx_ctx {
     int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
     bool shred_caps = false;           // tight caps sized for shredding windows (ccsx_gpu_run, shredded mode)
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
+    float mem_frac = 0.5f;             // of the device memory, the contexts sharing it use at most this fraction
     bool prealloc = false;             // reserve the slice budget up front
     bool bp_log = false;               // record the -v >= 3 breakpoint log (main.c:619-620)
     std::vector<uint32_t> run_bp;      // ccsx_gpu_run: the gathered logs, (i, ncols) pairs
@@ -732,7 +733,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         // ~7k mixed-size ZMWs, several times the resident workgroups, while
         // allocating up to the last free GB measured 6.3 s of staging for a
         // 305 GB slice vs 0.18 s for 84 GB
-        const uint64_t part = totb / (2ull * c->mem_share);
+        const uint64_t part = (uint64_t)((double)totb * c->mem_frac / c->mem_share);
         budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
     }
     // two slots in flight: each holds half
@@ -992,6 +993,13 @@ int ccsx_gpu_set_shred_read_cap(ccsx_ctx *c, uint32_t bases)
 {
     if (!c || bases < 1024 || bases > 65536) return -1;
     c->shred_read_cap = bases;
+    return 0;
+}
+
+int ccsx_gpu_set_mem_frac(ccsx_ctx *c, float frac)
+{
+    if (!c || !(frac > 0.05f && frac <= 0.95f)) return -1;
+    c->mem_frac = frac;
     return 0;
 }
 

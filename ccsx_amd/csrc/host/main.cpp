@@ -497,6 +497,7 @@ int main(int argc, char **argv)
     const int kcfg = getenv("CCSX_KCFG") ? atoi(getenv("CCSX_KCFG")) : -1;
     const int wg_cap = getenv("CCSX_WG_PER_CU") ? atoi(getenv("CCSX_WG_PER_CU")) : 0;
     const int read_cap = getenv("CCSX_SHRED_READ_CAP") ? atoi(getenv("CCSX_SHRED_READ_CAP")) : 0;
+    const float mem_frac = getenv("CCSX_MEM_FRAC") ? (float)atof(getenv("CCSX_MEM_FRAC")) : 0.f;
     for (int i = 0; i < nctx; ++i) {
         const int dev = (i / nslot) % ndev;
         if (ccsx_gpu_open(dev, &ctx[i]) != 0) return 1;
@@ -505,8 +506,9 @@ int main(int argc, char **argv)
         if (verbose > 2 && split_subread) ccsx_gpu_set_bp_log(ctx[i], 1);
         if ((kcfg >= 0 && ccsx_gpu_set_kernel_cfg(ctx[i], kcfg) != 0) ||
             (wg_cap > 0 && ccsx_gpu_set_wg_cap(ctx[i], (uint32_t)wg_cap) != 0) ||
-            (read_cap > 0 && ccsx_gpu_set_shred_read_cap(ctx[i], (uint32_t)read_cap) != 0)) {
-            fprintf(stderr, "[ccsx] invalid CCSX_KCFG / CCSX_WG_PER_CU / CCSX_SHRED_READ_CAP\n");
+            (read_cap > 0 && ccsx_gpu_set_shred_read_cap(ctx[i], (uint32_t)read_cap) != 0) ||
+            (mem_frac > 0.f && ccsx_gpu_set_mem_frac(ctx[i], mem_frac) != 0)) {
+            fprintf(stderr, "[ccsx] invalid CCSX_KCFG / CCSX_WG_PER_CU / CCSX_SHRED_READ_CAP / CCSX_MEM_FRAC\n");
             return 1;
         }
     }

@@ -28,7 +28,7 @@ EXPORTS = {
                    "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count",
                    "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for",
                    "ccsx_gpu_run_stats", "ccsx_gpu_zmw_bytes", "ccsx_gpu_set_slot_budget", "ccsx_gpu_set_wg_cap",
-                   "ccsx_gpu_set_shred_read_cap"],
+                   "ccsx_gpu_set_shred_read_cap", "ccsx_gpu_set_mem_frac"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
                     "ccsx_zmw_cost", "ccsx_partition",
@@ -88,6 +88,7 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_set_wg_cap.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_shred_read_cap.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_mem_share.argtypes = [C.c_void_p, C.c_uint32]
+        L.ccsx_gpu_set_mem_frac.argtypes = [C.c_void_p, C.c_float]
         L.ccsx_gpu_set_bp_log.argtypes = [C.c_void_p, C.c_int]
         L.ccsx_gpu_bp_log.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.POINTER(C.c_uint32)),
                                       C.POINTER(C.c_uint32)]

@@ -71,6 +71,10 @@ int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_
  * per GPU): cap this context's slices at total device memory / share
  * (default 1 = whatever is free). */
 int ccsx_gpu_set_mem_share(ccsx_ctx *ctx, uint32_t share);
+/* The fraction of the device memory all contexts sharing it may use together
+ * (default 0.5; 0.05 < frac <= 0.95): each context's slices are sized from
+ * total memory x frac / share, split over its two slots. */
+int ccsx_gpu_set_mem_frac(ccsx_ctx *ctx, float frac);
 /* on != 0: the first ccsx_gpu_run reserves the whole slice budget for the
  * workspace at once instead of growing it with the chunk size (re-allocating
  * a workspace a launch has touched costs ~30 ms per GB; a fresh one does
