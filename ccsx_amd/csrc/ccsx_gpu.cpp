@@ -235,6 +235,15 @@ struct ccsx_ctx {
     std::vector<uint64_t> run_bp_off;  // per ZMW of the call: offset into run_bp (pairs)
     std::vector<uint32_t> run_bp_n;    // per ZMW of the call: rounds
     std::vector<uint8_t> run_arena;    // ccsx_gpu_run's gathered CCS strings
+    // ccsx_gpu_submit / ccsx_gpu_collect: one batch per slot
+    struct Ticket {
+        bool pending = false;          // submitted, not collected
+        int mode = 0;
+        const ccsx_zmw_in *z = nullptr;  // the caller's batch (valid until collected)
+        size_t nz = 0;
+        int64_t fault = -1;            // test hook, taken from ccsx_gpu_set_fault at submit
+        std::vector<uint8_t> arena;    // the collected batch's CCS strings
+    } tk[2];
 };
 
 static int fail(ccsx_ctx *c, const char *what, hipError_t e)
@@ -689,6 +698,44 @@ int ccsx_gpu_fetch(ccsx_ctx *c, ccsx_zmw_out *out)
     return fetch_slot(c, c->slot[0], out);
 }
 
+// The bytes one slot's slice may take: what is free plus what the workspaces
+// already hold, at most this context's share of the device (mem_frac /
+// mem_share), halved for the two slots in flight; a preallocating context
+// reserves both slots' workspaces at that size on its first call.
+static int plan_slots(ccsx_ctx *c, uint64_t &slot_budget)
+{
+    size_t freeb = 0, totb = 0;
+    HIPCHK(c, hipMemGetInfo(&freeb, &totb));
+    // the workspaces may grow into what is free plus what they already hold;
+    // the sequence / output arenas they would need beside them stay counted
+    // as used (they are re-reserved per slice, not released)
+    const uint64_t held = c->slot[0].d_ws.cap + c->slot[1].d_ws.cap;
+    uint64_t budget = freeb + held > (3ull << 30) ? freeb + held - (3ull << 30) : (1ull << 30);
+    {
+        // a fixed share of the device per context (contexts running
+        // concurrently cannot all size themselves to the same free memory):
+        // allocating up to the last free GB measured 6.3 s of staging for a
+        // 305 GB slice vs 0.18 s for 84 GB (DESIGN.md section 7)
+        const uint64_t part = (uint64_t)((double)totb * c->mem_frac / c->mem_share);
+        budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
+    }
+    // two slots in flight: each holds half
+    slot_budget = c->slot_budget ? c->slot_budget : std::max<uint64_t>(1ull << 29, budget / 2);
+    if (c->prealloc) {
+        const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
+        for (Slot &s : c->slot)
+            if (s.d_ws.cap < slot_budget) {
+                const auto t0 = std::chrono::steady_clock::now();
+                HIPCHK(c, s.d_ws.reserve(slot_budget, true));
+                if (timing)
+                    fprintf(stderr, "[ccsx_gpu_run] dev %d: workspace of %.1f GB reserved in %.0f ms\n", c->device,
+                            slot_budget / 1e9,
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+            }
+    }
+    return 0;
+}
+
 // statuses of a tight-cap slice that the full-cap (uncapped read buffer) re-run clears
 static bool is_cap_error(int32_t s)
 {
@@ -714,43 +761,20 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             HIPCHK(c, hipStreamSynchronize(s.stream));
             s.inflight = false;
         }
+    c->tk[0].pending = c->tk[1].pending = false;  // (uncollected submitted batches are dropped)
     struct ShredCaps {  // the window-sized tight caps for this call only
         ccsx_ctx *c;
         ShredCaps(ccsx_ctx *x, bool on) : c(x) { c->shred_caps = on; }
         ~ShredCaps() { c->shred_caps = false; }
     } shred_caps(c, mode == CCSX_MODE_SHRED);
-    size_t freeb = 0, totb = 0;
-    HIPCHK(c, hipMemGetInfo(&freeb, &totb));
-    // the workspaces may grow into what is free plus what they already hold;
-    // the sequence / output arenas they would need beside them stay counted
-    // as used (they are re-reserved per slice, not released)
-    const uint64_t held = c->slot[0].d_ws.cap + c->slot[1].d_ws.cap;
-    uint64_t budget = freeb + held > (3ull << 30) ? freeb + held - (3ull << 30) : (1ull << 30);
+    uint64_t slot_budget = 0;
     {
-        // at most half the device per context (and a fixed share of it when
-        // contexts run concurrently, so they cannot both size themselves to
-        // the same free memory): a slice of half the device already holds
-        // ~7k mixed-size ZMWs, several times the resident workgroups, while
-        // allocating up to the last free GB measured 6.3 s of staging for a
-        // 305 GB slice vs 0.18 s for 84 GB (DESIGN.md section 7)
-        const uint64_t part = (uint64_t)((double)totb * c->mem_frac / c->mem_share);
-        budget = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(budget, part > (2ull << 30) ? part - (2ull << 30) : 0));
+        const int r = plan_slots(c, slot_budget);
+        if (r) return r;
     }
-    // two slots in flight: each holds half
-    const uint64_t slot_budget = c->slot_budget ? c->slot_budget : std::max<uint64_t>(1ull << 29, budget / 2);
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     using ms = std::chrono::duration<double, std::milli>;
     const auto t_run = std::chrono::steady_clock::now();
-    if (c->prealloc) {
-        for (Slot &s : c->slot)
-            if (s.d_ws.cap < slot_budget) {
-                const auto t0 = std::chrono::steady_clock::now();
-                HIPCHK(c, s.d_ws.reserve(slot_budget, true));
-                if (timing)
-                    fprintf(stderr, "[ccsx_gpu_run] dev %d: workspace of %.1f GB reserved in %.0f ms\n", c->device,
-                            slot_budget / 1e9, ms(std::chrono::steady_clock::now() - t0).count());
-            }
-    }
     c->run_arena.clear();
     c->run_bp.clear();
     c->run_bp_off.assign(nz, 0);
@@ -929,6 +953,166 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
     }
     c->fault = -1;
     for (size_t i = 0; i < nz; ++i) out[i].ccs = reinterpret_cast<const char *>(c->run_arena.data() + aoff[i]);
+    if (!first_err.empty()) {
+        c->err = first_err;
+        return -2;
+    }
+    return 0;
+}
+
+// Asynchronous batches: a batch that fits one slot runs as one launch on a
+// free slot; the caller submits its next batch before collecting the
+// previous one, so the device always holds the next launch (whose workgroups
+// fill the CUs the current launch's tail frees) and the host's staging and
+// gathering overlap the kernels -- where ccsx_gpu_run's callers wait for
+// every slice of a call before staging the next call.
+int ccsx_gpu_slot_bytes(ccsx_ctx *c, uint64_t *bytes)
+{
+    if (!c || !bytes) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    return plan_slots(c, *bytes);
+}
+
+int ccsx_gpu_submit(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, int *slot)
+{
+    if (!c || !slot || (!z && nz)) return -1;
+    if (mode != CCSX_MODE_SHRED && mode != CCSX_MODE_PRIMITIVE) {
+        c->err = "mode must be CCSX_MODE_SHRED or CCSX_MODE_PRIMITIVE";
+        return -1;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    int si = -1;
+    for (int k = 0; k < 2 && si < 0; ++k)
+        if (!c->tk[k].pending) si = k;
+    if (si < 0) {
+        c->err = "both slots hold batches not collected yet";
+        return -3;
+    }
+    Slot &s = c->slot[si];
+    if (s.inflight) {  // a stage/launch without fetch on this slot: drop its results
+        HIPCHK(c, hipStreamSynchronize(s.stream));
+        s.inflight = false;
+    }
+    uint64_t slot_budget = 0;
+    int r = plan_slots(c, slot_budget);
+    if (r) return r;
+    c->shred_caps = mode == CCSX_MODE_SHRED;
+    uint64_t tot = 0;
+    bool one_class = true;
+    for (size_t i = 0; i < nz; ++i) {
+        tot += zmw_bytes(z[i], false, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+        one_class = one_class && zmw_class(z[i], c->shred_caps) == zmw_class(z[0], c->shred_caps);
+    }
+    if (tot > slot_budget || !one_class) {
+        c->shred_caps = false;
+        char m[160];
+        snprintf(m, sizeof m, "batch of %.1f GB (%s) does not fit one %.1f GB slot: use ccsx_gpu_run", tot / 1e9,
+                 one_class ? "one launch class" : "several launch classes", slot_budget / 1e9);
+        c->err = m;
+        return -4;
+    }
+    r = stage_slot(c, s, z, nz, 0, 0);
+    if (!r) r = launch_slot(c, s, mode);
+    c->shred_caps = false;
+    if (r) return r;
+    ++c->slices;
+    c->tk[si].pending = true;
+    c->tk[si].mode = mode;
+    c->tk[si].z = z;
+    c->tk[si].nz = nz;
+    c->tk[si].fault = c->fault;
+    c->fault = -1;
+    *slot = si;
+    return 0;
+}
+
+int ccsx_gpu_collect(ccsx_ctx *c, int si, ccsx_zmw_out *out)
+{
+    if (!c || si < 0 || si > 1 || !c->tk[si].pending) {
+        if (c) c->err = "no batch submitted on that slot";
+        return -1;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    auto &t = c->tk[si];
+    Slot &s = c->slot[si];
+    const size_t nz = t.nz;
+    const ccsx_zmw_in *z = t.z;
+    t.pending = false;
+    std::vector<ccsx_zmw_out> o(nz);
+    int r = fetch_slot(c, s, o.data());
+    if (r && r != -2) return r;
+    std::vector<uint64_t> aoff(nz, 0);
+    std::vector<uint32_t> retry;
+    std::string first_err;
+    t.arena.clear();
+    auto gather = [&](const ccsx_zmw_out *res, const uint32_t *idx, size_t n, bool can_retry) {
+        size_t add = 0;
+        for (size_t i = 0; i < n; ++i) add += res[i].status ? 0 : res[i].len;
+        t.arena.reserve(t.arena.size() + add);
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t g = idx ? idx[i] : (uint32_t)i;
+            out[g].cells = res[i].cells;
+            out[g].status = res[i].status;
+            out[g].len = 0;
+            if (res[i].status) {
+                if (can_retry && is_cap_error(res[i].status)) {
+                    retry.push_back(g);
+                } else if (first_err.empty()) {
+                    char m[200];
+                    snprintf(m, sizeof m, "ZMW %u of the batch failed on the device: %s", g,
+                             ccsx_gpu_status_str(res[i].status));
+                    first_err = m;
+                }
+                continue;
+            }
+            aoff[g] = t.arena.size();
+            out[g].len = res[i].len;
+            t.arena.insert(t.arena.end(), res[i].ccs, res[i].ccs + res[i].len);
+        }
+    };
+    gather(o.data(), nullptr, nz, true);
+    if (!retry.empty()) {
+        // ZMWs that outgrew a tight cap: full caps, on this slot, slices of
+        // at most the slot budget (rare: none of 500,000 config-E ZMWs)
+        c->reruns += retry.size();
+        uint64_t slot_budget = 0;
+        r = plan_slots(c, slot_budget);
+        if (r) return r;
+        std::vector<uint32_t> todo;
+        todo.swap(retry);
+        std::vector<ccsx_zmw_in> sub;
+        c->shred_caps = t.mode == CCSX_MODE_SHRED;
+        for (size_t b = 0; b < todo.size() && !r;) {
+            uint64_t need = 0;
+            size_t e = b;
+            while (e < todo.size()) {
+                const uint64_t x = zmw_bytes(z[todo[e]], true, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+                if (e > b && need + x > slot_budget) break;
+                need += x;
+                ++e;
+            }
+            sub.resize(e - b);
+            for (size_t i = b; i < e; ++i) sub[i - b] = z[todo[i]];
+            r = stage_slot(c, s, sub.data(), sub.size(), 0, 1);
+            if (!r) r = launch_slot(c, s, t.mode);
+            if (!r) {
+                o.assign(sub.size(), ccsx_zmw_out{});
+                r = fetch_slot(c, s, o.data());
+                if (r == -2) r = 0;
+                if (!r) gather(o.data(), todo.data() + b, sub.size(), false);
+            }
+            ++c->slices;
+            b = e;
+        }
+        c->shred_caps = false;
+        if (r) return r;
+    }
+    if (t.fault >= 0 && (size_t)t.fault < nz) {
+        out[t.fault].status = ccsx::kErrTrace;
+        out[t.fault].len = 0;
+        if (first_err.empty()) first_err = "ZMW failed on the device: injected fault (test hook)";
+    }
+    for (size_t i = 0; i < nz; ++i) out[i].ccs = reinterpret_cast<const char *>(t.arena.data() + aoff[i]);
     if (!first_err.empty()) {
         c->err = first_err;
         return -2;

@@ -162,9 +162,10 @@ int usage()
             "Environment:\n"
             "CCSX_NGPU      Number of GPU contexts groups [all visible GPUs]; more than the visible\n"
             "               GPUs places group g on GPU g %% visible (logical contexts)\n"
-            "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
+            "CCSX_SLOTS     Device contexts (worker threads) per group [1; 2 with CCSX_ASYNC=0]\n"
+            "CCSX_ASYNC     0: one ccsx_gpu_run per batch instead of pipelined submit / collect [1]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
-            "CCSX_CHUNK     Largest chunk in ZMWs [8192 x contexts]\n"
+            "CCSX_CHUNK     Largest chunk in ZMWs [16384 x contexts; 8192 x contexts with CCSX_ASYNC=0]\n"
             "CCSX_CHUNK0    First chunk in ZMWs [CCSX_CHUNK / 2], growing x4 up to CCSX_CHUNK\n"
             "CCSX_KCFG      Force a kernel configuration (0 latency, 1 occupancy, 2 throughput, 3 solo)\n"
             "CCSX_DEV_SHARE Processes sharing each GPU [1] (each context's memory share shrinks)\n"
@@ -261,6 +262,15 @@ public:
     {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait(g, [this] { return closed_ || !q_.empty(); });
+        if (q_.empty()) return false;
+        b = std::move(q_.front());
+        q_.pop_front();
+        return true;
+    }
+    // without waiting: false if no batch is queued right now
+    bool try_pop(Batch &b)
+    {
+        std::lock_guard<std::mutex> g(m_);
         if (q_.empty()) return false;
         b = std::move(q_.front());
         q_.pop_front();
@@ -483,7 +493,13 @@ int main(int argc, char **argv)
     // two contexts per GPU: each pulls micro-batches on its own worker thread,
     // so one batch's staging and tail overlap the other's kernels (100k
     // config-E ZMWs: 10.66 s vs 12.12 s with one, profiles/r03)
-    int ngroup = ndev, nslot = 2;
+    // step 1 pipelined per context (ccsx_gpu_submit / ccsx_gpu_collect: the
+    // next batch is launched before the previous one is collected), one
+    // context per GPU; CCSX_ASYNC=0: ccsx_gpu_run per batch, two contexts per
+    // GPU overlapping each other (also for the -v >= 3 breakpoint log, which
+    // ccsx_gpu_run gathers)
+    const bool async = !(getenv("CCSX_ASYNC") && atoi(getenv("CCSX_ASYNC")) == 0) && !(verbose > 2 && split_subread);
+    int ngroup = ndev, nslot = async ? 1 : 2;
     if (const char *e = getenv("CCSX_NGPU")) ngroup = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("CCSX_SLOTS")) nslot = std::max(1, std::min(8, atoi(e)));
     const int nctx = ngroup * nslot;
@@ -542,51 +558,102 @@ int main(int argc, char **argv)
     const std::string fault_hole = getenv("CCSX_FAULT_HOLE") ? getenv("CCSX_FAULT_HOLE") : "";
 
     // step 1, device side: one worker per context
-    auto worker = [&](int w) {
+    // a batch in flight on a context: its input arrays live until collected
+    struct Flight {
         Batch b;
         std::vector<ccsx_zmw_in> in;
         std::vector<ccsx_zmw_out> out;
-        while (queue.pop(b)) {
-            Chunk &ch = *b.chunk;
-            if (!fatal) {
-                in.resize(b.idx.size());
-                out.assign(b.idx.size(), ccsx_zmw_out{});
-                for (size_t i = 0; i < b.idx.size(); ++i) {
-                    const Zmw &z = ch.zs[b.idx[i]];
-                    in[i] = ccsx_zmw_in{z.seqs, z.seg_off.data(), z.seg_len.data(), (uint32_t)z.seg_len.size()};
-                    if (!fault_hole.empty() && z.hole == fault_hole) ccsx_gpu_set_fault(ctx[w], (int64_t)i);
-                }
-                const double t0 = now_ms();
-                const int r = ccsx_gpu_run(ctx[w], mode, in.data(), in.size(), out.data());
-                if (r == 0 || r == -2) {
-                    // -2: some ZMWs failed on the device, the rest are valid
-                    uint64_t cells = 0;
-                    for (size_t i = 0; i < b.idx.size(); ++i) cells += out[i].cells;
-                    cells_total += cells;
-                    for (size_t i = 0; i < b.idx.size(); ++i) {
-                        Zmw &z = ch.zs[b.idx[i]];
-                        z.status = out[i].status;
-                        if (!out[i].status) z.ccs.assign(out[i].ccs, out[i].len);
-                        const uint32_t *lg;
-                        uint32_t nr = 0;
-                        if (verbose > 2 && !out[i].status && ccsx_gpu_bp_log(ctx[w], i, &lg, &nr) == 0)
-                            z.bp.assign(lg, lg + 2 * (size_t)nr);
-                    }
-                } else {
-                    std::lock_guard<std::mutex> g(err_m);
-                    fprintf(stderr, "[ccsx] device context %d: %s\n", w, ccsx_gpu_error(ctx[w]));
-                    fatal = true;
-                }
-                if (timing)
-                    fprintf(stderr, "[ccsx] chunk %zu batch of %zu ZMWs on context %d: %.0f-%.0f ms\n", ch.id,
-                            b.idx.size(), w, t0, now_ms());
+        int slot = -1;
+        double t0 = 0;
+    };
+    auto prepare_in = [&](int w, Flight &f) {
+        Chunk &ch = *f.b.chunk;
+        f.in.resize(f.b.idx.size());
+        f.out.assign(f.b.idx.size(), ccsx_zmw_out{});
+        for (size_t i = 0; i < f.b.idx.size(); ++i) {
+            const Zmw &z = ch.zs[f.b.idx[i]];
+            f.in[i] = ccsx_zmw_in{z.seqs, z.seg_off.data(), z.seg_len.data(), (uint32_t)z.seg_len.size()};
+            if (!fault_hole.empty() && z.hole == fault_hole) ccsx_gpu_set_fault(ctx[w], (int64_t)i);
+        }
+        f.t0 = now_ms();
+    };
+    // results of a batch (r: the run / collect status) into its chunk
+    auto finish = [&](int w, Flight &f, int r) {
+        Chunk &ch = *f.b.chunk;
+        if (r == 0 || r == -2) {
+            // -2: some ZMWs failed on the device, the rest are valid
+            uint64_t cells = 0;
+            for (size_t i = 0; i < f.b.idx.size(); ++i) cells += f.out[i].cells;
+            cells_total += cells;
+            for (size_t i = 0; i < f.b.idx.size(); ++i) {
+                Zmw &z = ch.zs[f.b.idx[i]];
+                z.status = f.out[i].status;
+                if (!f.out[i].status) z.ccs.assign(f.out[i].ccs, f.out[i].len);
+                const uint32_t *lg;
+                uint32_t nr = 0;
+                if (verbose > 2 && !f.out[i].status && ccsx_gpu_bp_log(ctx[w], i, &lg, &nr) == 0)
+                    z.bp.assign(lg, lg + 2 * (size_t)nr);
             }
-            const bool chunk_done = b.chunk->pending.fetch_sub(1) == 1;
-            ring.batch_done();
-            // the bases were staged: the arena goes back before the chunk is
-            // written (the writer needs only names and CCS)
-            if (chunk_done) b.chunk->release_arena();
-            b.chunk.reset();
+        } else if (!fatal.exchange(true)) {
+            std::lock_guard<std::mutex> g(err_m);
+            fprintf(stderr, "[ccsx] device context %d: %s\n", w, ccsx_gpu_error(ctx[w]));
+        }
+        if (timing)
+            fprintf(stderr, "[ccsx] chunk %zu batch of %zu ZMWs on context %d: %.0f-%.0f ms\n", ch.id, f.b.idx.size(),
+                    w, f.t0, now_ms());
+        const bool chunk_done = f.b.chunk->pending.fetch_sub(1) == 1;
+        ring.batch_done();
+        // the bases were staged: the arena goes back before the chunk is
+        // written (the writer needs only names and CCS)
+        if (chunk_done) f.b.chunk->release_arena();
+        f.b.chunk.reset();
+    };
+    auto worker = [&](int w) {
+        if (!async) {
+            Flight f;
+            while (queue.pop(f.b)) {
+                if (fatal) {
+                    finish(w, f, -1);
+                    continue;
+                }
+                prepare_in(w, f);
+                finish(w, f, ccsx_gpu_run(ctx[w], mode, f.in.data(), f.in.size(), f.out.data()));
+            }
+            return;
+        }
+        // pipelined: up to two batches in flight, the next one submitted
+        // before the oldest is collected (include/ccsx_gpu.h)
+        std::deque<Flight> fl;
+        for (;;) {
+            Flight f;
+            const bool got = fl.size() < 2 && (fl.empty() ? queue.pop(f.b) : queue.try_pop(f.b));
+            if (got) {
+                if (fatal) {
+                    finish(w, f, -1);
+                    continue;
+                }
+                prepare_in(w, f);
+                const int r = ccsx_gpu_submit(ctx[w], mode, f.in.data(), f.in.size(), &f.slot);
+                if (r == -4) {
+                    // larger than a slot: collect what is in flight, then
+                    // the batch through ccsx_gpu_run's slices
+                    while (!fl.empty()) {
+                        Flight &g = fl.front();
+                        finish(w, g, ccsx_gpu_collect(ctx[w], g.slot, g.out.data()));
+                        fl.pop_front();
+                    }
+                    finish(w, f, ccsx_gpu_run(ctx[w], mode, f.in.data(), f.in.size(), f.out.data()));
+                } else if (r != 0) {
+                    finish(w, f, r);
+                } else {
+                    fl.push_back(std::move(f));
+                }
+                continue;
+            }
+            if (fl.empty()) break;  // the queue is closed and empty
+            Flight &g = fl.front();
+            finish(w, g, ccsx_gpu_collect(ctx[w], g.slot, g.out.data()));
+            fl.pop_front();
         }
     };
     std::vector<std::thread> workers;
@@ -639,7 +706,15 @@ int main(int argc, char **argv)
     // r03o)
     uint32_t batches_per_ctx = 1;
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    size_t chunk_max = std::min<size_t>(8192u * (size_t)nctx, 262144u);
+    // (pipelined contexts: 16,384 ZMWs each, one launch per chunk and GPU)
+    size_t chunk_max = std::min<size_t>((async ? 16384u : 8192u) * (size_t)nctx, 262144u);
+    // pipelined: batches of at most ~95 % of a slot (ccsx_gpu_slot_bytes),
+    // so a submitted batch always fits one launch
+    uint64_t slot_bytes = 0;
+    if (async && ccsx_gpu_slot_bytes(ctx[0], &slot_bytes) != 0) {
+        fprintf(stderr, "[ccsx] device context 0: %s\n", ccsx_gpu_error(ctx[0]));
+        return 1;
+    }
     if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));
     // step 0's reading on its own thread, one chunk ahead of the preparation
     // (the reference's step 0 does both in turn: main.c:652-697)
@@ -699,8 +774,17 @@ int main(int argc, char **argv)
         std::vector<uint64_t> cost(n);
         for (uint32_t i = 0; i < n; ++i) cost[i] = ccsx_zmw_cost(zs[i].seg_len.data(), (uint32_t)zs[i].seg_len.size());
         std::vector<uint32_t> order(n), bounds(n + 1);
-        const uint32_t nb = ccsx_partition(cost.data(), n, (uint32_t)nctx * batches_per_ctx, 256u, order.data(),
-                                           bounds.data());
+        uint32_t nparts = (uint32_t)nctx * batches_per_ctx;
+        if (async) {
+            uint64_t bytes = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                const ccsx_zmw_in zi{zs[i].seqs, zs[i].seg_off.data(), zs[i].seg_len.data(), (uint32_t)zs[i].seg_len.size()};
+                bytes += ccsx_gpu_zmw_bytes(ctx[0], mode, &zi);
+            }
+            const uint64_t per = slot_bytes / 20 * 19;
+            nparts = std::max<uint32_t>(nparts, (uint32_t)((bytes + per - 1) / std::max<uint64_t>(per, 1)));
+        }
+        const uint32_t nb = ccsx_partition(cost.data(), n, nparts, 256u, order.data(), bounds.data());
         std::vector<Batch> bs(nb);
         for (uint32_t b = 0; b < nb; ++b) {
             bs[b].chunk = ch;

@@ -28,7 +28,8 @@ EXPORTS = {
                    "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count",
                    "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for",
                    "ccsx_gpu_run_stats", "ccsx_gpu_zmw_bytes", "ccsx_gpu_set_slot_budget", "ccsx_gpu_set_wg_cap",
-                   "ccsx_gpu_set_shred_read_cap", "ccsx_gpu_set_mem_frac"],
+                   "ccsx_gpu_set_shred_read_cap", "ccsx_gpu_set_mem_frac",
+                   "ccsx_gpu_slot_bytes", "ccsx_gpu_submit", "ccsx_gpu_collect"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
                     "ccsx_zmw_cost", "ccsx_partition",
@@ -89,6 +90,9 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_set_shred_read_cap.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_mem_share.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_mem_frac.argtypes = [C.c_void_p, C.c_float]
+        L.ccsx_gpu_slot_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.ccsx_gpu_submit.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwIn), C.c_size_t, C.POINTER(C.c_int)]
+        L.ccsx_gpu_collect.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwOut)]
         L.ccsx_gpu_set_bp_log.argtypes = [C.c_void_p, C.c_int]
         L.ccsx_gpu_bp_log.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.POINTER(C.c_uint32)),
                                       C.POINTER(C.c_uint32)]
@@ -403,6 +407,35 @@ class Engine:
         """Device bytes one ZMW occupies in a ccsx_gpu_run slice of `mode`."""
         arr, keep = self._build_in([z])
         return int(self._L.ccsx_gpu_zmw_bytes(self._ctx, mode, arr))
+
+    def slot_bytes(self) -> int:
+        """ccsx_gpu_slot_bytes: the bytes one submitted batch may take."""
+        v = C.c_uint64(0)
+        if self._L.ccsx_gpu_slot_bytes(self._ctx, C.byref(v)) != 0:
+            self._err("ccsx_gpu_slot_bytes")
+        return int(v.value)
+
+    def submit(self, zmws: list, mode: int = MODE_SHRED) -> int:
+        """ccsx_gpu_submit: stage + launch one batch on a free slot (returns
+        the slot to collect; raises on -3 / -4 with the code in the message)."""
+        arr, keep = self._build_in(zmws)
+        slot = C.c_int(-1)
+        rc = self._L.ccsx_gpu_submit(self._ctx, mode, arr, len(zmws), C.byref(slot))
+        if rc != 0:
+            self._err(f"ccsx_gpu_submit ({rc})")
+        self._tickets = getattr(self, "_tickets", {})
+        self._tickets[slot.value] = (arr, keep, len(zmws))
+        return slot.value
+
+    def collect(self, slot: int):
+        """ccsx_gpu_collect: [(ccs bytes, status, cells)] of a submitted batch."""
+        arr, keep, n = self._tickets.pop(slot)
+        out = (ZmwOut * max(n, 1))()
+        rc = self._L.ccsx_gpu_collect(self._ctx, slot, out)
+        if rc not in (0, -2):
+            self._err("ccsx_gpu_collect")
+        return [(C.string_at(out[i].ccs, out[i].len) if out[i].len else b"", out[i].status, out[i].cells)
+                for i in range(n)]
 
     def set_bp_log(self, on: bool = True) -> None:
         """Record the -v >= 3 breakpoint log (main.c:619-620) in ccsx_gpu_run."""

@@ -67,6 +67,22 @@ const char *ccsx_gpu_status_str(int32_t status);
  * Returns 0, -2 (some ZMWs failed, see out[i].status) or -1. */
 int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zmw_out *out);
 
+/* Pipelined batches (the host program's step 1): ccsx_gpu_submit stages a
+ * batch that fits one slot into a free slot of the context's two and launches
+ * it without waiting; ccsx_gpu_collect waits for that slot's batch and
+ * returns its results (ZMWs that outgrew a tight cap re-run with full caps
+ * inside the collect).  Submitting the next batch before collecting the
+ * previous keeps the device fed.  *slot: the ticket to collect.  The
+ * caller's input arrays must stay valid until the collect; out[i].ccs is
+ * valid until that slot's next collect.  submit returns -3 when both slots
+ * hold uncollected batches and -4 when the batch does not fit one slot
+ * (ccsx_gpu_slot_bytes; or mixes launch classes): run it with ccsx_gpu_run
+ * once the submitted batches are collected (ccsx_gpu_run drops uncollected
+ * ones).  collect returns 0, -2 (some ZMWs failed) or -1. */
+int ccsx_gpu_slot_bytes(ccsx_ctx *ctx, uint64_t *bytes);
+int ccsx_gpu_submit(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, int *slot);
+int ccsx_gpu_collect(ccsx_ctx *ctx, int slot, ccsx_zmw_out *out);
+
 /* Contexts sharing one device concurrently (the CLI keeps two chunks in flight
  * per GPU): cap this context's slices at total device memory / share
  * (default 1 = whatever is free). */

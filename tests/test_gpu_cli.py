@@ -49,35 +49,38 @@ def test_cli_matches_oracle(tmp_path, mode_flag, mode):
     assert got.count(b">") == 10
 
 
-def test_cli_multi_chunk_order(tmp_path):
-    """1,100 ZMWs: more than the first 1,024-ZMW chunk (main.c:686-690), so the
-    second chunk is read and prepared while the GPU runs the first; the output
-    stays in input order and equal to the oracle's."""
+@pytest.mark.parametrize("async_", ["1", "0"])
+def test_cli_multi_chunk_order(tmp_path, async_):
+    """1,100 ZMWs in chunks of at most 1,024 (CCSX_CHUNK; the first is half
+    of it), so later chunks are read and prepared while the GPU runs the
+    first; pipelined submit / collect (CCSX_ASYNC=1, with three batches per
+    chunk so batches of the next chunk are submitted before the previous are
+    collected) and one ccsx_gpu_run per batch: the output stays in input order
+    and equal to the oracle's."""
     fa = str(tmp_path / "in.fa")
     write(fa, 1100, 1000, 6)
     out = str(tmp_path / "out.fa")
-    r = subprocess.run([BIN, "-A", "-j", "4", fa, out], capture_output=True, timeout=300)
-    assert r.returncode == 0, r.stderr.decode()
+    _run(["-A", "-j", "4", fa, out], env=dict(CCSX_CHUNK="1024", CCSX_ASYNC=async_, CCSX_CTX_BATCHES="3"))
     got = open(out, "rb").read()
     assert got.count(b">") == 1100
     assert got == _expected(fa, 0)
 
 
 def test_cli_logical_contexts_match_one(tmp_path):
-    """Three chunks (1,024 + 4,096 + 180 ZMWs) split into cost-balanced
-    micro-batches over N >= 2 device contexts (CCSX_NGPU groups beyond the
-    visible GPUs are logical contexts on the same device):
-    byte-identical to one context, in input order (main.c:701-704,707-717),
-    and equal to the oracle."""
+    """Chunks of at most 2,048 ZMWs split into cost-balanced micro-batches
+    over N >= 2 device contexts (CCSX_NGPU groups beyond the visible GPUs are
+    logical contexts on the same device), pipelined or one
+    ccsx_gpu_run per batch: byte-identical to one context, in input order
+    (main.c:701-704,707-717), and equal to the oracle."""
     fa = str(tmp_path / "in.fa")
     write(fa, 5300, 1000, 6)
     outs = []
-    for ngpu, slots in (("1", "1"), ("3", "2"), ("2", "1")):
-        out = str(tmp_path / f"out{ngpu}_{slots}.fa")
-        _run(["-A", "-j", "8", fa, out], env=dict(CCSX_NGPU=ngpu, CCSX_SLOTS=slots))
+    for ngpu, slots, async_ in (("1", "1", "1"), ("3", "2", "1"), ("2", "1", "0"), ("1", "2", "0")):
+        out = str(tmp_path / f"out{ngpu}_{slots}_{async_}.fa")
+        _run(["-A", "-j", "8", fa, out], env=dict(CCSX_NGPU=ngpu, CCSX_SLOTS=slots, CCSX_ASYNC=async_, CCSX_CHUNK="2048"))
         outs.append(open(out, "rb").read())
     assert outs[0].count(b">") == 5300
-    assert outs[1] == outs[0] and outs[2] == outs[0]
+    assert all(o == outs[0] for o in outs[1:])
     assert outs[0] == _expected(fa, 0)
 
 

@@ -369,3 +369,37 @@ def test_multi_slice_run(engine):
     finally:
         engine.set_slot_budget(0)
         engine.set_bp_log(False)
+
+
+def test_submit_collect_pipeline(engine):
+    """ccsx_gpu_submit / ccsx_gpu_collect: two batches in flight on the two
+    slots, a third submit refused (-3) until one is collected, a ZMW whose
+    window outgrows the read cap re-run with full caps inside its collect,
+    results in input order and equal to the oracle; a batch larger than a
+    slot is refused (-4)."""
+    zs1 = [synth(8100 + h, 2000, 8) for h in range(12)]
+    zs2 = [synth(8200 + h, 3000, 6) for h in range(9)] + [synth(7500, 12000, 2)]
+    want1, _, _ = batch(zs1, cx.MODE_SHRED, 8)
+    want2, _, _ = batch(zs2, cx.MODE_SHRED, 8)
+    before = engine.rerun_count()
+    s1 = engine.submit(zs1)
+    s2 = engine.submit(zs2)
+    assert s1 != s2
+    with pytest.raises(cx.GpuError, match=r"\(-3\)"):
+        engine.submit(zs1)
+    g1 = engine.collect(s1)
+    s3 = engine.submit(zs1[:5])
+    g2 = engine.collect(s2)
+    g3 = engine.collect(s3)
+    assert [g for g, st, _ in g1] == want1 and all(st == 0 for _, st, _ in g1)
+    assert [g for g, st, _ in g2] == want2 and all(st == 0 for _, st, _ in g2)
+    assert [g for g, _, _ in g3] == want1[:5]
+    assert engine.rerun_count() - before >= 1
+    engine.set_slot_budget(1 << 20)
+    try:
+        with pytest.raises(cx.GpuError, match=r"\(-4\)"):
+            engine.submit(zs1)
+    finally:
+        engine.set_slot_budget(0)
+    # ccsx_gpu_run still works on the same context afterwards
+    assert [g for g, _, _ in engine.run(zs1[:3], cx.MODE_SHRED)] == want1[:3]
