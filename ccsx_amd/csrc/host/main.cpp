@@ -162,7 +162,7 @@ int usage()
             "Environment:\n"
             "CCSX_NGPU      Number of GPU contexts groups [all visible GPUs]; more than the visible\n"
             "               GPUs places group g on GPU g %% visible (logical contexts)\n"
-            "CCSX_SLOTS     Device contexts (worker threads) per group [1; 2 with CCSX_ASYNC=0]\n"
+            "CCSX_SLOTS     Device contexts (worker threads) per group [2]\n"
             "CCSX_ASYNC     0: one ccsx_gpu_run per batch instead of pipelined submit / collect [1]\n"
             "CCSX_TIMING    1: per-chunk / per-batch timing on stderr\n"
             "CCSX_CHUNK     Largest chunk in ZMWs [16384 x contexts; 8192 x contexts with CCSX_ASYNC=0]\n"
@@ -494,12 +494,14 @@ int main(int argc, char **argv)
     // so one batch's staging and tail overlap the other's kernels (100k
     // config-E ZMWs: 10.66 s vs 12.12 s with one, profiles/r03)
     // step 1 pipelined per context (ccsx_gpu_submit / ccsx_gpu_collect: the
-    // next batch is launched before the previous one is collected), one
-    // context per GPU; CCSX_ASYNC=0: ccsx_gpu_run per batch, two contexts per
-    // GPU overlapping each other (also for the -v >= 3 breakpoint log, which
-    // ccsx_gpu_run gathers)
+    // next batch is launched before the previous one is collected);
+    // CCSX_ASYNC=0: one ccsx_gpu_run per batch (also for the -v >= 3
+    // breakpoint log, which ccsx_gpu_run gathers)
     const bool async = !(getenv("CCSX_ASYNC") && atoi(getenv("CCSX_ASYNC")) == 0) && !(verbose > 2 && split_subread);
-    int ngroup = ndev, nslot = async ? 1 : 2;
+    // two contexts per GPU either way: pipelined, each keeps two launches in
+    // flight (200k config-E ZMWs: 9.4-9.7 s with two contexts, 10.7 s with
+    // one, 9.9-10.0 s for two contexts of ccsx_gpu_run; gpurun_out r04r/r04s)
+    int ngroup = ndev, nslot = 2;
     if (const char *e = getenv("CCSX_NGPU")) ngroup = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("CCSX_SLOTS")) nslot = std::max(1, std::min(8, atoi(e)));
     const int nctx = ngroup * nslot;
@@ -707,7 +709,7 @@ int main(int argc, char **argv)
     uint32_t batches_per_ctx = 1;
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
     // (pipelined contexts: 16,384 ZMWs each, one launch per chunk and GPU)
-    size_t chunk_max = std::min<size_t>((async ? 16384u : 8192u) * (size_t)nctx, 262144u);
+    size_t chunk_max = std::min<size_t>((async ? 16384u : 8192u) * (size_t)nctx, 131072u);
     // pipelined: batches of at most ~95 % of a slot (ccsx_gpu_slot_bytes),
     // so a submitted batch always fits one launch
     uint64_t slot_bytes = 0;
