@@ -2052,6 +2052,9 @@ __device__ __forceinline__ uint32_t col_end(const uint8_t *nb, uint32_t v, uint3
 // in HBM.  LM = 0: larger graphs (-P) take the same steps through HBM.
 __device__ __forceinline__ int merge_in_lds(uint32_t R)
 {
+#ifdef CCSX_MERGE_NO_LDS  // measurement variant (LDS bank-conflict attribution)
+    return 0 * R;
+#endif
     constexpr uint32_t bytes = (uint32_t)(kRingA * kRowW * 4);
     return (R + 1) * 5u + 64u <= bytes ? 2 : R + 64u <= bytes ? 1 : 0;
 }
