@@ -14,7 +14,11 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session", autouse=True)
 def _built():
-    """Build the native libraries once per session (incremental, no GPU needed)."""
+    """Build the native libraries once per session (incremental, no GPU needed;
+    CCSX_NO_BUILD=1: use the libraries as they are, e.g. a variant under test)."""
+    if os.environ.get("CCSX_NO_BUILD"):
+        yield
+        return
     from ccsx_amd.build import build_oracle, build_product
     build_product()
     build_oracle()

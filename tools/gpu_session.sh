@@ -45,8 +45,8 @@ step() {
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gputest.log" 2>&1
       local rc=$?; tail -3 "$OUT/gputest.log"; return $rc ;;
     parity)
-      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/parity.log" 2>&1
-      local rc=$?; tail -3 "$OUT/parity.log"; return $rc ;;
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/parity${CCSX_LIB:+_$CCSX_LIB}.log" 2>&1
+      local rc=$?; tail -3 "$OUT/parity${CCSX_LIB:+_$CCSX_LIB}.log"; return $rc ;;
     bench)
       if [ -z "$cfg" ]; then
         timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" && cat "$OUT/bench.json"
