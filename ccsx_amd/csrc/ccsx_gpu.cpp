@@ -973,6 +973,17 @@ int ccsx_gpu_slot_bytes(ccsx_ctx *c, uint64_t *bytes)
     return plan_slots(c, *bytes);
 }
 
+int ccsx_gpu_reserve_staging(ccsx_ctx *c, uint64_t seq_bytes, uint64_t out_bytes)
+{
+    if (!c) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    for (Slot &s : c->slot) {
+        HIPCHK(c, s.h_seq.reserve(seq_bytes));
+        HIPCHK(c, s.h_out.reserve(out_bytes));
+    }
+    return 0;
+}
+
 int ccsx_gpu_submit(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, int *slot)
 {
     if (!c || !slot || (!z && nz)) return -1;

@@ -537,6 +537,13 @@ int main(int argc, char **argv)
         }
     }
 
+    // pipelined: batches of at most ~95 % of a slot (ccsx_gpu_slot_bytes),
+    // so a submitted batch always fits one launch
+    uint64_t slot_bytes = 0;
+    if (async && ccsx_gpu_slot_bytes(ctx[0], &slot_bytes) != 0) {
+        fprintf(stderr, "[ccsx] device context 0: %s\n", ccsx_gpu_error(ctx[0]));
+        return 1;
+    }
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     const auto tstart = std::chrono::steady_clock::now();
     if (timing)
@@ -554,6 +561,7 @@ int main(int argc, char **argv)
     ChunkRing ring(3);
     std::atomic<bool> fatal(false);
     std::atomic<uint64_t> cells_total(0);  // DP cells the devices computed (CCSX_TIMING report)
+    std::atomic<int> workers_busy(0);      // pipelined workers still running
     std::mutex err_m;
 
     // test hook: the device reports this hole as failed (tests/test_gpu_cli.py)
@@ -624,7 +632,11 @@ int main(int argc, char **argv)
             return;
         }
         // pipelined: up to two batches in flight, the next one submitted
-        // before the oldest is collected (include/ccsx_gpu.h)
+        // before the oldest is collected (include/ccsx_gpu.h).  First the
+        // pinned staging of both slots, sized for a slot's batch (subreads
+        // and CCS slabs are ~1/56 of a config-E slot each), while step 0
+        // still reads the first chunk
+        if (slot_bytes) (void)ccsx_gpu_reserve_staging(ctx[w], slot_bytes / 48, slot_bytes / 48);
         std::deque<Flight> fl;
         for (;;) {
             Flight f;
@@ -657,8 +669,16 @@ int main(int argc, char **argv)
             finish(w, g, ccsx_gpu_collect(ctx[w], g.slot, g.out.data()));
             fl.pop_front();
         }
+        // a context with no more work releases its pinned staging and device
+        // memory while the others run their last batches (≈ 0.2 s each that
+        // the process exit would otherwise pay); the last one is left to it
+        if (!fatal && workers_busy.fetch_sub(1) > 1) {
+            ccsx_gpu_close(ctx[w]);
+            ctx[w] = nullptr;
+        }
     };
     std::vector<std::thread> workers;
+    workers_busy = nctx;
     for (int w = 0; w < nctx; ++w) workers.emplace_back(worker, w);
 
     // step 2: ordered output (main.c:707-717)
@@ -710,13 +730,6 @@ int main(int argc, char **argv)
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
     // (pipelined contexts: 16,384 ZMWs each, one launch per chunk and GPU)
     size_t chunk_max = std::min<size_t>((async ? 16384u : 8192u) * (size_t)nctx, 131072u);
-    // pipelined: batches of at most ~95 % of a slot (ccsx_gpu_slot_bytes),
-    // so a submitted batch always fits one launch
-    uint64_t slot_bytes = 0;
-    if (async && ccsx_gpu_slot_bytes(ctx[0], &slot_bytes) != 0) {
-        fprintf(stderr, "[ccsx] device context 0: %s\n", ccsx_gpu_error(ctx[0]));
-        return 1;
-    }
     if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));
     // step 0's reading on its own thread, one chunk ahead of the preparation
     // (the reference's step 0 does both in turn: main.c:652-697)

@@ -29,7 +29,7 @@ EXPORTS = {
                    "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for",
                    "ccsx_gpu_run_stats", "ccsx_gpu_zmw_bytes", "ccsx_gpu_set_slot_budget", "ccsx_gpu_set_wg_cap",
                    "ccsx_gpu_set_shred_read_cap", "ccsx_gpu_set_mem_frac",
-                   "ccsx_gpu_slot_bytes", "ccsx_gpu_submit", "ccsx_gpu_collect"],
+                   "ccsx_gpu_slot_bytes", "ccsx_gpu_submit", "ccsx_gpu_collect", "ccsx_gpu_reserve_staging"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
                     "ccsx_zmw_cost", "ccsx_partition",

@@ -80,6 +80,11 @@ int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_
  * once the submitted batches are collected (ccsx_gpu_run drops uncollected
  * ones).  collect returns 0, -2 (some ZMWs failed) or -1. */
 int ccsx_gpu_slot_bytes(ccsx_ctx *ctx, uint64_t *bytes);
+/* Reserve both slots' pinned host staging (subreads, CCS) up front, e.g. on
+ * a worker thread while the first batch is still being read, instead of in
+ * the first batch's staging (~0.2 s per GB: huge-page mapping, touch,
+ * registration). */
+int ccsx_gpu_reserve_staging(ccsx_ctx *ctx, uint64_t seq_bytes, uint64_t out_bytes);
 int ccsx_gpu_submit(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, int *slot);
 int ccsx_gpu_collect(ccsx_ctx *ctx, int slot, ccsx_zmw_out *out);
 
