@@ -303,9 +303,22 @@ __device__ __forceinline__ bool win_has(uint32_t c0, uint32_t nc, int32_t off)
 __device__ __forceinline__ uint32_t rd_win16(const Z &z, int32_t off, bool inwin)
 {
     const uint32_t b = ((uint32_t)off + 2u * lane_id()) >> 2;
+#ifdef CCSX_RD_ALIGN
+    // the aligned dwords holding bytes b, b + 1, funnel-shifted (no unaligned
+    // 16-bit LDS access)
+    const uint32_t w = b >> 2, sh = (b & 3u) * 8u;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(z.rd);
+    if (z.hbm && inwin) {
+        const uint32_t *win = reinterpret_cast<const uint32_t *>(z.win);
+        constexpr uint32_t wm = kRdWinBytes / 4 - 1;
+        return __builtin_amdgcn_alignbit(win[(w + 1) & wm], win[w & wm], sh);
+    }
+    return __builtin_amdgcn_alignbit(src[w + 1], src[w], sh);
+#else
     if (!z.hbm) return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
     if (inwin) return (uint32_t)z.win[b & kWinBytesMask] | (uint32_t)z.win[(b + 1) & kWinBytesMask] << 8;
     return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
+#endif
 }
 
 // the codes of read positions off + d + 2 lane (bits 0-1) and the next (bits
@@ -996,7 +1009,7 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
 // predecessor / D beat M, per cell; X = H' + 2 t; Pex = the insertion scan's
 // exclusive prefix max.  maybe_wide: the row may have more than 63
 // predecessors (its slots also go to the wide slot records).
-template <bool FULL, bool TRACK = true>
+template <bool FULL>
 __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, int32_t &bOff,
                                            const __amdgpu_buffer_rsrc_t &rc, uint32_t r, uint32_t m, int32_t lim,
                                            int32_t off, uint32_t np, bool maybe_wide, const PredAcc &A, const LaneK &c,
@@ -1018,27 +1031,21 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
             make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
     }
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
-    // H' at j = m - 1 (!TRACK: the caller tracks them, dpS_row)
-    if (!FULL) {
-        if ((uint32_t)c.L2 >= m) w0 = 0;
-        if ((uint32_t)c.L2 + 1 >= m) w1 = 0;
+    // H' at j = m - 1
+    const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
+    int32_t e0 = X0 + eb;
+    int32_t e1 = X1 + eb;
+    if (FULL) {
+        e1 += (off == lim && lane == 63) ? 3 : 0;
+    } else {
+        if ((uint32_t)c.L2 == m - 1) e0 += 3;
+        if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
+        if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
+        if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
     }
-    if (TRACK) {
-        const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
-        int32_t e0 = X0 + eb;
-        int32_t e1 = X1 + eb;
-        if (FULL) {
-            e1 += (off == lim && lane == 63) ? 3 : 0;
-        } else {
-            if ((uint32_t)c.L2 == m - 1) e0 += 3;
-            if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
-            if ((uint32_t)c.L2 >= m) e0 = INT32_MIN;
-            if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN;
-        }
-        // rows come in order: the first maximum is the earliest (min row, min cell)
-        if (e0 > bE) bE = e0, bKey = r * 2, bOff = off;
-        if (e1 > bE) bE = e1, bKey = r * 2 + 1, bOff = off;
-    }
+    // rows come in order: the first maximum is the earliest (min row, min cell)
+    if (e0 > bE) bE = e0, bKey = r * 2, bOff = off;
+    if (e1 > bE) bE = e1, bKey = r * 2 + 1, bOff = off;
     // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
     __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
                                           0);
@@ -1264,11 +1271,9 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
 // bit the same records.
 // ----------------------------------------------------------------------------
 struct SolB {
-    int32_t bE;       // !FULL: best free-end value of this lane's cells
+    int32_t bE;       // best free-end value of this lane's cells
     uint32_t bKey;    // its row * 2 + cell
     int32_t bOff;     // its row's band offset
-    int32_t sE;       // FULL: the best free-end value so far (uniform), its row and read position
-    uint32_t sRow, sJ;
     __amdgpu_buffer_rsrc_t rc;  // cell records of this DP (R rows x 256 B)
 };
 
@@ -1300,14 +1305,7 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         const bool d0 = Dv0 > M0, d1 = Dv1 > M1;
         const int32_t hp0 = max(M0, Dv0), hp1 = max(M1, Dv1);
         const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
-        // FULL: the insertion scan runs on keys X << 7 | (127 - t), so its
-        // lane 63 is also the row's largest X = H' + 2t and its first cell:
-        // the row's free-end candidate (SPEC.md §3.5) becomes one readlane
-        // and a few scalar ops instead of per-lane tracking.  X < 2^24 in
-        // magnitude on valid cells (|H'| <= 2m + O(1), m < 2^22), so the key
-        // is exact and Pex = key >> 7; lane 0's exclusive value INT32_MIN >>
-        // 7 is as far below every H' as kNeg is (nothing it meets changes)
-        int32_t incl = FULL ? max((X0 << 7) | c.kc0, (X1 << 7) | c.kc1) : max(X0, X1);
+        int32_t incl = max(X0, X1);
         int32_t rk0 = (hp0 << 7) | c.kc0, rk1 = (hp1 << 7) | c.kc1;
         if (!FULL) {
             if ((uint32_t)c.L2 >= m) rk0 = INT32_MIN, Dv0 = kNeg;
@@ -1315,21 +1313,7 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         }
         int32_t rk = max(rk0, rk1);
         wave_incl_max2(incl, rk);
-        const int32_t Pex = FULL ? (wave_shr1(INT32_MIN, incl) >> 7) : wave_shr1(kNeg, incl);
-        if (FULL) {
-            // the first maximum of e = X + 2 off - 2m - 1 over the row's
-            // cells, H' at j = m - 1 (cell 127 when off == lim) counting + 3;
-            // rows come in order, so a later row wins only if strictly better
-            const int32_t kx = __builtin_amdgcn_readlane(incl, 63);
-            const int32_t eb = 2 * off - 2 * (int32_t)m - 1;
-            int32_t e = (kx >> 7) + eb;
-            uint32_t t = 127u - (uint32_t)(kx & 127);
-            if (off == lim) {
-                const int32_t xb = __builtin_amdgcn_readlane(X1, 63) + eb + 3;
-                if (xb > e) e = xb, t = 127u;
-            }
-            if (e > B.sE) B.sE = e, B.sRow = r, B.sJ = (uint32_t)off + t;
-        }
+        const int32_t Pex = wave_shr1(kNeg, incl);
         const int32_t ex1 = max(Pex, X0);
         int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(ex1 + c.cI1, hp1);
         if (!FULL) {
@@ -1359,7 +1343,7 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         S.pArg = off + 127 - (key & 127);
         // decision bits, free-end candidates, record (only a cold row can
         // have more than 63 predecessors)
-        row_record<FULL, !FULL>(z, B.bE, B.bKey, B.bOff, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0,
+        row_record<FULL>(z, B.bE, B.bKey, B.bOff, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0,
                          X1, Pex);
     };
     if (__builtin_expect(fast, 1)) {
@@ -1447,7 +1431,6 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     S.W.nxt = S.W.cur;
     SolB B;
     B.bE = INT32_MIN, B.bKey = 0, B.bOff = 0;
-    B.sE = INT32_MIN, B.sRow = 0, B.sJ = 0;
     B.rc = brsrc(z.ws + z.L.codes, z.R * 256u);
     const uint32_t nblk = dp_nblk(z.R);
     for (uint32_t b = 0; b < nblk && !z.status; ++b) {
@@ -1462,18 +1445,13 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
         }
     }
     // the candidate: lexicographic (max score, min row, min j)
-    if (FULL) {
-        er_out = B.sE == INT32_MIN ? 0xFFFFFFFFu : B.sRow;
-        ej_out = B.sJ;
-    } else {
-        const int32_t best = wave_max(B.bE);
-        const uint32_t rsel = B.bE == best ? B.bKey >> 1 : 0x7FFFFFFFu;
-        const int32_t rmin = wave_min((int32_t)rsel);
-        const bool mine = B.bE == best && (B.bKey >> 1) == (uint32_t)rmin;
-        const int32_t jsel = mine ? B.bOff + 2 * lane + (int32_t)(B.bKey & 1u) : INT32_MAX;
-        er_out = best == INT32_MIN ? 0xFFFFFFFFu : (uint32_t)rmin;
-        ej_out = (uint32_t)wave_min(jsel);
-    }
+    const int32_t best = wave_max(B.bE);
+    const uint32_t rsel = B.bE == best ? B.bKey >> 1 : 0x7FFFFFFFu;
+    const int32_t rmin = wave_min((int32_t)rsel);
+    const bool mine = B.bE == best && (B.bKey >> 1) == (uint32_t)rmin;
+    const int32_t jsel = mine ? B.bOff + 2 * lane + (int32_t)(B.bKey & 1u) : INT32_MAX;
+    er_out = best == INT32_MIN ? 0xFFFFFFFFu : (uint32_t)rmin;
+    ej_out = (uint32_t)wave_min(jsel);
     wsync();  // records and row meta in HBM before the traceback's DMA reads them
     z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
 }
