@@ -88,11 +88,11 @@ struct HostBuf {
     }
     // at least `floor` bytes (the CLI's contexts pin their staging once:
     // re-pinning a grown arena costs ~0.25 s per GB)
-    hipError_t reserve(size_t n, size_t floor = 0)
+    hipError_t reserve(size_t n, size_t floor = 0, bool exact = false)
     {
         if (n <= cap) return hipSuccess;
         release();
-        size_t c = std::max<size_t>(std::max<size_t>(n + n / 4, floor), 4096);
+        size_t c = std::max<size_t>(std::max<size_t>(exact ? n : n + n / 4, floor), 4096);
         {
             // an anonymous mapping with transparent huge pages, touched, then
             // registered with HIP: pinning and (at the process exit)
@@ -225,6 +225,7 @@ struct ccsx_ctx {
     uint64_t dealt = 0, parts = 0;     // lists ccsx_gpu_run dealt into interleaved parts, and their parts
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
+    uint32_t tight_out = 0;            // test hook: override the tight output slab
     int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
     bool shred_caps = false;           // tight caps sized for shredding windows (ccsx_gpu_run, shredded mode)
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
@@ -376,13 +377,13 @@ static void zmw_extent(const ccsx_zmw_in &zi, uint64_t &S, uint64_t &hi, uint32_
 }
 
 // device bytes one ZMW occupies when staged
-static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, uint32_t tight_rows, uint32_t shred_win)
+static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, const ccsx_ctx *c, uint32_t shred_win)
 {
     uint64_t S, hi;
     uint32_t lmax;
     zmw_extent(zi, S, hi, lmax);
     ccsx::ZmwDesc d{};
-    ccsx::zcaps(d, S, lmax, zi.nseg, full, tight_rows, shred_win);
+    ccsx::zcaps(d, S, lmax, zi.nseg, full, c->tight_rows, shred_win, c->tight_out);
     ccsx::ZLayout L;
     ccsx::zlayout(L, d);
     return ccsx::align256(L.total) + hi + d.outcap + uint64_t(zi.nseg) * 8 + sizeof(ccsx::ZmwDesc) + 32;
@@ -411,7 +412,8 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
             return -1;
         }
         ccsx::ZmwDesc &d = s.desc[i];
-        ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+        ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u,
+                    c->tight_out);
         d.seg0 = nseg;
         d.seq_off = seq_b;
         seq_b += hi;
@@ -740,7 +742,7 @@ static int plan_slots(ccsx_ctx *c, uint64_t &slot_budget)
 static bool is_cap_error(int32_t s)
 {
     return s == ccsx::kErrRows || s == ccsx::kErrEdges || s == ccsx::kErrMulti || s == ccsx::kErrSpill ||
-           s == ccsx::kErrReadLen || s == ccsx::kErrBpLog;
+           s == ccsx::kErrReadLen || s == ccsx::kErrBpLog || s == ccsx::kErrOut;
 }
 
 // One chunk.  The chunk is cut into slices that fit the device's free memory
@@ -861,7 +863,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             std::vector<uint64_t> xb(idx0.size());
             uint64_t tot = 0, xmax = 0;
             for (size_t i = 0; i < idx0.size(); ++i) {
-                xb[i] = zmw_bytes(z[idx0[i]], full, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+                xb[i] = zmw_bytes(z[idx0[i]], full, c, c->shred_caps ? c->shred_read_cap : 0u);
                 tot += xb[i];
                 xmax = std::max(xmax, xb[i]);
             }
@@ -891,7 +893,7 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
             uint64_t need = 0;
             size_t e = b;
             while (e < idx.size()) {
-                const uint64_t x = zmw_bytes(z[idx[e]], full, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+                const uint64_t x = zmw_bytes(z[idx[e]], full, c, c->shred_caps ? c->shred_read_cap : 0u);
                 if (e > b && (need + x > slot_budget || cls[idx[e]] != cls[idx[b]] || e == cut)) break;
                 need += x;
                 ++e;
@@ -977,9 +979,13 @@ int ccsx_gpu_reserve_staging(ccsx_ctx *c, uint64_t seq_bytes, uint64_t out_bytes
 {
     if (!c) return -1;
     HIPCHK(c, hipSetDevice(c->device));
-    for (Slot &s : c->slot) {
-        HIPCHK(c, s.h_seq.reserve(seq_bytes));
-        HIPCHK(c, s.h_out.reserve(out_bytes));
+    // the slot the next submit takes; exact sizes (a later batch grows them)
+    for (int k = 0; k < 2; ++k) {
+        if (c->tk[k].pending) continue;
+        Slot &s = c->slot[k];
+        HIPCHK(c, s.h_seq.reserve(seq_bytes, 0, true));
+        HIPCHK(c, s.h_out.reserve(out_bytes, 0, true));
+        break;
     }
     return 0;
 }
@@ -1011,7 +1017,7 @@ int ccsx_gpu_submit(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, int 
     uint64_t tot = 0;
     bool one_class = true;
     for (size_t i = 0; i < nz; ++i) {
-        tot += zmw_bytes(z[i], false, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+        tot += zmw_bytes(z[i], false, c, c->shred_caps ? c->shred_read_cap : 0u);
         one_class = one_class && zmw_class(z[i], c->shred_caps) == zmw_class(z[0], c->shred_caps);
     }
     if (tot > slot_budget || !one_class) {
@@ -1097,7 +1103,7 @@ int ccsx_gpu_collect(ccsx_ctx *c, int si, ccsx_zmw_out *out)
             uint64_t need = 0;
             size_t e = b;
             while (e < todo.size()) {
-                const uint64_t x = zmw_bytes(z[todo[e]], true, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u);
+                const uint64_t x = zmw_bytes(z[todo[e]], true, c, c->shred_caps ? c->shred_read_cap : 0u);
                 if (e > b && need + x > slot_budget) break;
                 need += x;
                 ++e;
@@ -1138,6 +1144,13 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *c, uint32_t rows)
     return 0;
 }
 
+int ccsx_gpu_set_tight_out(ccsx_ctx *c, uint32_t bytes)
+{
+    if (!c) return -1;
+    c->tight_out = bytes;
+    return 0;
+}
+
 int ccsx_gpu_set_kernel_cfg(ccsx_ctx *c, int cfg)
 {
     if (!c || cfg < -1 || cfg >= ccsx::kCfgCount) return -1;
@@ -1160,7 +1173,7 @@ int ccsx_gpu_run_stats(const ccsx_ctx *c, uint64_t *st, uint32_t n)
 uint64_t ccsx_gpu_zmw_bytes(const ccsx_ctx *c, int mode, const ccsx_zmw_in *z)
 {
     if (!c || !z) return 0;
-    return zmw_bytes(*z, false, c->tight_rows, mode == CCSX_MODE_SHRED ? c->shred_read_cap : 0u);
+    return zmw_bytes(*z, false, c, mode == CCSX_MODE_SHRED ? c->shred_read_cap : 0u);
 }
 
 int ccsx_gpu_set_fault(ccsx_ctx *c, int64_t zmw)

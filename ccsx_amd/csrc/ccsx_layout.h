@@ -190,9 +190,12 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 // are of 2 kb windows (+2 kb per missed breakpoint) rather than whole
 // segments, so the tight row cap follows the window, not the segment (rows ~
 // window x (1 + ~0.07 reads): 3 x 4,096 + 4,096 covers 4 kb windows of up to
-// ~40 reads).  0: not shredded.
+// ~40 reads).  0: not shredded.  The output slab: S + 16 bytes bound any
+// consensus (one base per column, columns <= S); tight caps hold 2 x the
+// longest segment + 1,024 (a CCS is about one insert long; kErrOut re-runs
+// the ZMW uncapped), tight_out overriding (tests).
 CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, bool full = true,
-                          uint32_t tight_rows = 0, uint32_t shred_win = 0)
+                          uint32_t tight_rows = 0, uint32_t shred_win = 0, uint32_t tight_out = 0)
 {
     d.n = n;
     d.rcap = uint32_t(S + 16);
@@ -213,6 +216,10 @@ CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, boo
     // only ZMWs of >= 65 segments can have rows above 63 predecessors
     d.wcap = n > 64 ? d.rcap : 0;
     d.outcap = uint32_t(S + 16);
+    if (!full) {
+        const uint64_t oc = tight_out ? tight_out : 2ull * lmax + 1024;
+        if (oc < d.outcap) d.outcap = uint32_t(oc);
+    }
 }
 
 struct KArgs {

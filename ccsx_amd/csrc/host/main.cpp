@@ -482,32 +482,22 @@ int main(int argc, char **argv)
         fprintf(stderr, "Cannot open file for write!\n");
         return 1;
     }
-    const int ndev = ccsx_gpu_device_count();
-    if (ndev <= 0) {
-        fprintf(stderr, "[ccsx] no HIP device: the MI355X engine needs a GPU\n");
-        return 1;
-    }
-    // CCSX_NGPU groups of CCSX_SLOTS contexts; group g on device g % ndev
-    // (more groups than devices: logical contexts sharing a device, which is
-    // how the multi-GPU split is exercised on a one-GPU box)
-    // two contexts per GPU: each pulls micro-batches on its own worker thread,
-    // so one batch's staging and tail overlap the other's kernels (100k
-    // config-E ZMWs: 10.66 s vs 12.12 s with one, profiles/r03)
     // step 1 pipelined per context (ccsx_gpu_submit / ccsx_gpu_collect: the
     // next batch is launched before the previous one is collected);
     // CCSX_ASYNC=0: one ccsx_gpu_run per batch (also for the -v >= 3
     // breakpoint log, which ccsx_gpu_run gathers)
     const bool async = !(getenv("CCSX_ASYNC") && atoi(getenv("CCSX_ASYNC")) == 0) && !(verbose > 2 && split_subread);
-    // two contexts per GPU either way: pipelined, each keeps two launches in
-    // flight (200k config-E ZMWs: 9.4-9.7 s with two contexts, 10.7 s with
-    // one, 9.9-10.0 s for two contexts of ccsx_gpu_run; gpurun_out r04r/r04s)
-    int ngroup = ndev, nslot = 2;
-    if (const char *e = getenv("CCSX_NGPU")) ngroup = std::max(1, std::min(64, atoi(e)));
+    // CCSX_NGPU groups of CCSX_SLOTS contexts; group g on device g % ndev
+    // (more groups than devices: logical contexts sharing a device, which is
+    // how the multi-GPU split is exercised on a one-GPU box).  Two contexts
+    // per GPU: each pulls micro-batches on its own worker thread, so one
+    // batch's staging and tail overlap the other's kernels (100k config-E
+    // ZMWs: 10.66 s vs 12.12 s with one, profiles/r03); pipelined, each keeps
+    // two launches in flight (200k config-E ZMWs: 9.4-9.7 s with two
+    // contexts, 10.7 s with one, 9.9-10.0 s for two contexts of ccsx_gpu_run;
+    // gpurun_out r04r/r04s)
+    int nslot = 2;
     if (const char *e = getenv("CCSX_SLOTS")) nslot = std::max(1, std::min(8, atoi(e)));
-    const int nctx = ngroup * nslot;
-    std::vector<ccsx_ctx *> ctx(nctx, nullptr);
-    std::vector<int> per_dev(ndev, 0);
-    for (int i = 0; i < nctx; ++i) per_dev[(i / nslot) % ndev]++;
     // processes sharing each device (bench.py's multi-rank rehearsal on one
     // GPU): each context's memory share shrinks by that factor
     int dev_share = 1;
@@ -522,39 +512,22 @@ int main(int argc, char **argv)
     // longest-first order balances better (200k config-E ZMWs 11.0 s -> 10.0 s,
     // gpurun_out r04q); CCSX_MEM_FRAC overrides
     const float mem_frac = getenv("CCSX_MEM_FRAC") ? (float)atof(getenv("CCSX_MEM_FRAC")) : 0.85f;
-    for (int i = 0; i < nctx; ++i) {
-        const int dev = (i / nslot) % ndev;
-        if (ccsx_gpu_open(dev, &ctx[i]) != 0) return 1;
-        ccsx_gpu_set_mem_share(ctx[i], (uint32_t)(per_dev[dev] * dev_share));
-        ccsx_gpu_set_prealloc(ctx[i], 1);
-        if (verbose > 2 && split_subread) ccsx_gpu_set_bp_log(ctx[i], 1);
-        if ((kcfg >= 0 && ccsx_gpu_set_kernel_cfg(ctx[i], kcfg) != 0) ||
-            (wg_cap > 0 && ccsx_gpu_set_wg_cap(ctx[i], (uint32_t)wg_cap) != 0) ||
-            (read_cap > 0 && ccsx_gpu_set_shred_read_cap(ctx[i], (uint32_t)read_cap) != 0) ||
-            (mem_frac > 0.f && ccsx_gpu_set_mem_frac(ctx[i], mem_frac) != 0)) {
-            fprintf(stderr, "[ccsx] invalid CCSX_KCFG / CCSX_WG_PER_CU / CCSX_SHRED_READ_CAP / CCSX_MEM_FRAC\n");
-            return 1;
-        }
-    }
-
-    // pipelined: batches of at most ~95 % of a slot (ccsx_gpu_slot_bytes),
-    // so a submitted batch always fits one launch
-    uint64_t slot_bytes = 0;
-    if (async && ccsx_gpu_slot_bytes(ctx[0], &slot_bytes) != 0) {
-        fprintf(stderr, "[ccsx] device context 0: %s\n", ccsx_gpu_error(ctx[0]));
-        return 1;
-    }
+    // micro-batches per context and chunk (CCSX_CTX_BATCHES, default 1: 100k
+    // config-E ZMWs from the generator's pipe 15.2 s with 2, 11.8 s with 1,
+    // r03o)
+    uint32_t batches_per_ctx = 1;
+    if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     const auto tstart = std::chrono::steady_clock::now();
-    if (timing)
-        fprintf(stderr, "[ccsx] %d device context(s) open at %.0f ms after main (main at epoch %.3f s)\n", nctx,
-                std::chrono::duration<double, std::milli>(tstart - tmain).count(),
-                std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count() -
-                    std::chrono::duration<double>(std::chrono::steady_clock::now() - tmain).count());
     auto now_ms = [tstart]() {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tstart).count();
     };
     const int mode = split_subread ? CCSX_MODE_SHRED : CCSX_MODE_PRIMITIVE;
+    // the device contexts, opened on their own thread (below) while step 0
+    // reads and prepares the first chunk
+    int nctx = 0;
+    std::vector<ccsx_ctx *> ctx;
+    uint64_t slot_bytes = 0;
 
     ArenaPool arenas;  // (declared before every holder of a chunk)
     BatchQueue queue;
@@ -618,6 +591,16 @@ int main(int argc, char **argv)
         if (chunk_done) f.b.chunk->release_arena();
         f.b.chunk.reset();
     };
+    // workers whose batches are all finished (the output and the exit wait
+    // for this, not for a worker's teardown of its context)
+    std::mutex done_m;
+    std::condition_variable done_cv;
+    int nwork_done = 0;
+    auto work_done = [&](int) {
+        std::lock_guard<std::mutex> g(done_m);
+        ++nwork_done;
+        done_cv.notify_all();
+    };
     auto worker = [&](int w) {
         if (!async) {
             Flight f;
@@ -629,14 +612,16 @@ int main(int argc, char **argv)
                 prepare_in(w, f);
                 finish(w, f, ccsx_gpu_run(ctx[w], mode, f.in.data(), f.in.size(), f.out.data()));
             }
+            workers_busy.fetch_sub(1);
+            work_done(w);
             return;
         }
         // pipelined: up to two batches in flight, the next one submitted
         // before the oldest is collected (include/ccsx_gpu.h).  First the
-        // pinned staging of both slots, sized for a slot's batch (subreads
-        // and CCS slabs are ~1/56 of a config-E slot each), while step 0
-        // still reads the first chunk
-        if (slot_bytes) (void)ccsx_gpu_reserve_staging(ctx[w], slot_bytes / 48, slot_bytes / 48);
+        // pinned staging of the first slot, sized for a batch (a config-E
+        // batch's subreads are ~1/60 of a slot, its tight CCS slabs ~1/3 of
+        // that), while step 0 still reads the first chunk
+        if (slot_bytes) (void)ccsx_gpu_reserve_staging(ctx[w], slot_bytes / 56, slot_bytes / 160);
         std::deque<Flight> fl;
         for (;;) {
             Flight f;
@@ -671,22 +656,134 @@ int main(int argc, char **argv)
         }
         // a context with no more work releases its pinned staging and device
         // memory while the others run their last batches (≈ 0.2 s each that
-        // the process exit would otherwise pay); the last one is left to it
-        if (!fatal && workers_busy.fetch_sub(1) > 1) {
+        // the process exit would otherwise pay); the last one is left to it.
+        // The output waits for the work, not for the release (work_done)
+        const bool last = workers_busy.fetch_sub(1) == 1;
+        work_done(w);
+        if (!fatal && !last) {
             ccsx_gpu_close(ctx[w]);
             ctx[w] = nullptr;
         }
     };
     std::vector<std::thread> workers;
-    workers_busy = nctx;
-    for (int w = 0; w < nctx; ++w) workers.emplace_back(worker, w);
+
+    // step 0 (main.c:652-697) on its own thread, one chunk ahead of the
+    // preparation (the reference's step 0 does both in turn), started before
+    // the devices open: HIP's initialisation (~0.1 s) overlaps the first
+    // chunk's read.  The reference grows the chunk 1,024 -> 4,096 -> 16,384
+    // ZMWs (main.c:686-690); here the sizes scale with the device contexts
+    // (known once the devices are counted: until then the first chunk keeps
+    // growing; the sizes change only how the work is cut, never the output)
+    std::atomic<size_t> chunk_first(SIZE_MAX), chunk_last(SIZE_MAX);
+    ReadQueue rq(1);
+    std::thread reader([&]() {
+        size_t chunk_size = 0;
+        for (size_t id = 0;; ++id) {
+            auto ch = std::make_shared<Chunk>();
+            ch->id = id;
+            ch->pool = &arenas;
+            std::vector<Zmw> &zs = ch->zs;
+            ch->t_read0 = now_ms();
+            ccsx_ingest::ZmwRef zr;
+            int l;
+            while (!fatal && (l = rd->next(zr)) >= 0) {
+                if (l < min_fulllen_count + 2) continue;
+                const uint64_t total = zr.total();
+                if (total > (uint64_t)max_subread_len || total < (uint64_t)min_subread_len) continue;
+                if (have_holes && hole_set.count(zr.hole)) continue;
+                zs.emplace_back();
+                zs.back().ref = std::move(zr);
+                const size_t lim = chunk_size ? chunk_size : chunk_first.load();
+                if (zs.size() >= lim) {
+                    chunk_size = std::min(zs.size() * 4, chunk_last.load());
+                    break;
+                }
+            }
+            ch->t_read1 = now_ms();
+            // kt_pipeline stops on an empty chunk (main.c:694-697); a chunk
+            // cut short by -1 (end of input or an invalid name) is processed
+            // and the next read goes on, as the reference's next step 0 does
+            const bool last = zs.empty();
+            rq.push(std::move(ch));
+            if (last) {
+                arenas.drain();
+                break;
+            }
+        }
+    });
+    // the devices: contexts opened, their workers started (each reserves its
+    // first pinned staging at once); a failure ends the process here, before
+    // any output
+    std::thread opener([&]() {
+        auto die = [&](const char *what) {
+            fprintf(stderr, "[ccsx] %s\n", what);
+            fflush(stderr);
+            std::_Exit(1);
+        };
+        const int ndev = ccsx_gpu_device_count();
+        if (ndev <= 0) die("no HIP device: the MI355X engine needs a GPU");
+        int ngroup = ndev;
+        if (const char *e = getenv("CCSX_NGPU")) ngroup = std::max(1, std::min(64, atoi(e)));
+        const int n = ngroup * nslot;
+        // the last chunk size: 16,384 ZMWs per pipelined context (one launch
+        // per chunk and context), 8,192 per ccsx_gpu_run context (two slices
+        // of ~4,096, above the solo configuration's threshold, also with 8
+        // GPUs x 2 contexts); the first half of it (the reference starts at
+        // 1,024 ZMWs, main.c:686-690, which here only fed small launches on
+        // the latency / occupancy objects while the device idled: 62,500
+        // config-E ZMWs 6.3 s with 1,024, 5.4 s with 8,192, 5.8 s with 16,384,
+        // r04e); CCSX_CHUNK / CCSX_CHUNK0 override
+        size_t cmax = std::min<size_t>((async ? 16384u : 8192u) * (size_t)n, 131072u);
+        if (const char *e = getenv("CCSX_CHUNK")) cmax = std::max<size_t>(1024, strtoull(e, nullptr, 10));
+        size_t c0 = std::max<size_t>(1024, cmax / 2);
+        if (const char *e = getenv("CCSX_CHUNK0")) c0 = std::max<size_t>(1, std::min<size_t>(cmax, strtoull(e, nullptr, 10)));
+        chunk_last = cmax;
+        chunk_first = c0;
+        ctx.assign(n, nullptr);
+        std::vector<int> per_dev(ndev, 0);
+        for (int i = 0; i < n; ++i) per_dev[(i / nslot) % ndev]++;
+        for (int i = 0; i < n; ++i) {
+            const int dev = (i / nslot) % ndev;
+            if (ccsx_gpu_open(dev, &ctx[i]) != 0) die("cannot open a device context");
+            ccsx_gpu_set_mem_share(ctx[i], (uint32_t)(per_dev[dev] * dev_share));
+            ccsx_gpu_set_prealloc(ctx[i], 1);
+            if (verbose > 2 && split_subread) ccsx_gpu_set_bp_log(ctx[i], 1);
+            if ((kcfg >= 0 && ccsx_gpu_set_kernel_cfg(ctx[i], kcfg) != 0) ||
+                (wg_cap > 0 && ccsx_gpu_set_wg_cap(ctx[i], (uint32_t)wg_cap) != 0) ||
+                (read_cap > 0 && ccsx_gpu_set_shred_read_cap(ctx[i], (uint32_t)read_cap) != 0) ||
+                (mem_frac > 0.f && ccsx_gpu_set_mem_frac(ctx[i], mem_frac) != 0))
+                die("invalid CCSX_KCFG / CCSX_WG_PER_CU / CCSX_SHRED_READ_CAP / CCSX_MEM_FRAC");
+        }
+        // pipelined: batches of at most ~95 % of a slot (ccsx_gpu_slot_bytes),
+        // so a submitted batch always fits one launch
+        if (async && ccsx_gpu_slot_bytes(ctx[0], &slot_bytes) != 0) die(ccsx_gpu_error(ctx[0]));
+        if (timing)
+            fprintf(stderr, "[ccsx] %d device context(s) open at %.0f ms (main at epoch %.3f s, %.0f ms before)\n", n,
+                    now_ms(),
+                    std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count() -
+                        std::chrono::duration<double>(std::chrono::steady_clock::now() - tmain).count(),
+                    std::chrono::duration<double, std::milli>(tstart - tmain).count());
+        nctx = n;
+        workers_busy = n;
+        for (int w = 0; w < n; ++w) workers.emplace_back(worker, w);
+    });
+    bool opened = false;
+    auto await_open = [&]() {
+        if (!opened) opener.join();
+        opened = true;
+    };
 
     // step 2: ordered output (main.c:707-717)
     size_t nfail = 0;
-    // the last chunk written stays referenced here: freeing a chunk (~2 GB of
-    // per-ZMW strings) takes a few hundred ms, which mid-run overlaps the next
-    // chunk but at the end would only delay the exit (see the end of main)
+    // the last chunk written stays referenced here and the ones before it are
+    // freed on a thread of their own: freeing a chunk (its per-ZMW vectors and
+    // strings, the input blocks it holds) takes up to a few hundred ms, which
+    // would delay the next chunk's records and, at the end, the exit
     std::shared_ptr<Chunk> last_written;
+    ReadQueue reap(1 << 20);
+    std::thread reaper([&]() {
+        while (auto ch = reap.pop()) ch.reset();
+    });
     std::thread writer([&]() {
         while (auto ch = ring.next_done()) {
             if (!fatal && verbose > 2) {
@@ -711,71 +808,14 @@ int main(int argc, char **argv)
                 }
             }
             if (timing) fprintf(stderr, "[ccsx] chunk %zu written at %.0f ms\n", ch->id, now_ms());
-            last_written = ch;  // (frees the previous one)
+            if (last_written) reap.push(std::move(last_written));
+            last_written = ch;
             ring.pop();
         }
     });
 
-    // step 0 (main.c:652-697) + the CPU half of step 1; the reference grows
-    // the chunk 1,024 -> 4,096 -> 16,384 ZMWs (main.c:686-690), here the
-    // last size scales with the device contexts (output order does not
-    // depend on it): 8,192 ZMWs per context, so that each context's batch,
-    // cut into its two slots' slices, still holds ~4,096 ZMWs per launch --
-    // above the solo configuration's threshold (3 x the occupancy object's
-    // resident ZMWs, 3,840 on config E) -- also with 8 GPUs x 2 contexts.
-    // micro-batches per context and chunk (CCSX_CTX_BATCHES, default 1: 100k
-    // config-E ZMWs from the generator's pipe 15.2 s with 2, 11.8 s with 1,
-    // r03o)
-    uint32_t batches_per_ctx = 1;
-    if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    // (pipelined contexts: 16,384 ZMWs each, one launch per chunk and GPU)
-    size_t chunk_max = std::min<size_t>((async ? 16384u : 8192u) * (size_t)nctx, 131072u);
-    if (const char *e = getenv("CCSX_CHUNK")) chunk_max = std::max<size_t>(1024, strtoull(e, nullptr, 10));
-    // step 0's reading on its own thread, one chunk ahead of the preparation
-    // (the reference's step 0 does both in turn: main.c:652-697)
-    ReadQueue rq(1);
-    // first chunk: half the largest (the reference starts at 1,024 ZMWs,
-    // main.c:686-690, which here only fed small launches on the latency /
-    // occupancy objects while the device idled: 62,500 config-E ZMWs 6.3 s
-    // with 1,024, 5.4 s with 8,192, 5.8 s with 16,384, r04e; CCSX_CHUNK0
-    // overrides -- the chunk sizes change only how the work is cut, never
-    // the output)
-    size_t chunk0 = std::max<size_t>(1024, chunk_max / 2);
-    if (const char *e = getenv("CCSX_CHUNK0")) chunk0 = std::max<size_t>(1, std::min<size_t>(chunk_max, strtoull(e, nullptr, 10)));
-    std::thread reader([&]() {
-        size_t chunk_size = chunk0;
-        for (size_t id = 0;; ++id) {
-            auto ch = std::make_shared<Chunk>();
-            ch->id = id;
-            ch->pool = &arenas;
-            std::vector<Zmw> &zs = ch->zs;
-            ch->t_read0 = now_ms();
-            ccsx_ingest::ZmwRef zr;
-            int l;
-            while (!fatal && (l = rd->next(zr)) >= 0) {
-                if (l < min_fulllen_count + 2) continue;
-                const uint64_t total = zr.total();
-                if (total > (uint64_t)max_subread_len || total < (uint64_t)min_subread_len) continue;
-                if (have_holes && hole_set.count(zr.hole)) continue;
-                zs.emplace_back();
-                zs.back().ref = std::move(zr);
-                if (zs.size() >= chunk_size) {
-                    chunk_size = std::min(chunk_size * 4, chunk_max);
-                    break;
-                }
-            }
-            ch->t_read1 = now_ms();
-            // kt_pipeline stops on an empty chunk (main.c:694-697); a chunk
-            // cut short by -1 (end of input or an invalid name) is processed
-            // and the next read goes on, as the reference's next step 0 does
-            const bool last = zs.empty();
-            rq.push(std::move(ch));
-            if (last) {
-                arenas.drain();
-                break;
-            }
-        }
-    });
+    // the CPU half of step 1: each chunk prepared, cost-ordered and cut into
+    // micro-batches for the workers
     for (;;) {
         auto ch = rq.pop();
         if (ch->zs.empty() || fatal) break;
@@ -783,6 +823,7 @@ int main(int argc, char **argv)
         const size_t id = ch->id;
         const double t0 = ch->t_read0, t1 = ch->t_read1;
         prepare_chunk(*ch, nthreads, verbose);
+        await_open();
         // cost-balanced micro-batches: cost ranks dealt round-robin, each
         // batch longest first (dispatch.cpp)
         const uint32_t n = (uint32_t)zs.size();
@@ -815,15 +856,20 @@ int main(int argc, char **argv)
     // at the end of the input the reader has pushed its empty chunk and
     // returned; after a fatal device error it stops at its next record and
     // pushes without waiting for space
+    await_open();
     rq.stop();
     reader.join();
     ring.finish();
     queue.close();
-    for (auto &t : workers) t.join();
+    {
+        std::unique_lock<std::mutex> g(done_m);
+        done_cv.wait(g, [&] { return nwork_done == nctx; });
+    }
     if (fatal) ring.stop();
     writer.join();
     const double tw = now_ms();
     if (!fatal) {
+        // (a worker may still be releasing its context: the exit ends it)
         // every byte is written: flush and leave without tearing down the
         // device contexts (≈ 0.8 s of hipFree / hipHostFree for a 100k run)
         // or the last chunk; process exit releases both
@@ -833,10 +879,13 @@ int main(int argc, char **argv)
         if (werr) fprintf(stderr, "[ccsx] error writing the output: %s\n", strerror(errno));
         if (getenv("CCSX_EXIT_CLOSE")) {  // measurement: the teardown steps the exit skips, timed
             const double a = now_ms();
+            for (auto &t : workers) t.join();
             for (auto *x : ctx) ccsx_gpu_close(x);
             const double b = now_ms();
             rd.reset();
             const double d = now_ms();
+            reap.push(nullptr);
+            reaper.join();
             last_written.reset();
             std::string mem;
             if (FILE *f = fopen("/proc/self/smaps_rollup", "r")) {
@@ -857,7 +906,10 @@ int main(int argc, char **argv)
         fflush(stderr);
         std::_Exit(werr ? 1 : 0);
     }
+    for (auto &t : workers) t.join();
     for (auto *x : ctx) ccsx_gpu_close(x);
+    reap.push(nullptr);
+    reaper.join();
     if (timing) fprintf(stderr, "[ccsx] output done at %.0f ms, contexts closed at %.0f ms\n", tw, now_ms());
     rd.reset();
     if (fp_out != stdout) (void)fclose(fp_out);

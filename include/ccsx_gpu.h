@@ -80,10 +80,11 @@ int ccsx_gpu_run(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_
  * once the submitted batches are collected (ccsx_gpu_run drops uncollected
  * ones).  collect returns 0, -2 (some ZMWs failed) or -1. */
 int ccsx_gpu_slot_bytes(ccsx_ctx *ctx, uint64_t *bytes);
-/* Reserve both slots' pinned host staging (subreads, CCS) up front, e.g. on
- * a worker thread while the first batch is still being read, instead of in
- * the first batch's staging (~0.2 s per GB: huge-page mapping, touch,
- * registration). */
+/* Reserve the pinned host staging (subreads, CCS; exactly these sizes) of
+ * the slot the next submit takes, e.g. on a worker thread while the first
+ * batch is still being read, instead of in that batch's staging (huge-page
+ * mapping, touch, registration: ~0.1 s per GB).  The other slot's is sized by
+ * its first batch, while the first one's kernel runs. */
 int ccsx_gpu_reserve_staging(ccsx_ctx *ctx, uint64_t seq_bytes, uint64_t out_bytes);
 int ccsx_gpu_submit(ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z, size_t nz, int *slot);
 int ccsx_gpu_collect(ccsx_ctx *ctx, int slot, ccsx_zmw_out *out);
@@ -133,6 +134,9 @@ int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
  * 4096, the segment capped at the 4,096-base window read buffer in shredded
  * mode). */
 int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
+/* Test hook: tight output slab override in bytes (0 = default 2 x longest
+ * segment + 1,024; a consensus beyond it re-runs the ZMW with full caps). */
+int ccsx_gpu_set_tight_out(ccsx_ctx *ctx, uint32_t bytes);
 /* Kernel configuration of the next slices: -1 (default) = by slice size (the
  * latency configuration 0 -- three waves, 8-row DP blocks, 32-row LDS ring --
  * when it keeps the whole slice resident; the solo configuration 3 -- one

@@ -147,6 +147,25 @@ def test_capacity_rerun(engine, mode):
         engine.set_tight_rows(0)
 
 
+@pytest.mark.parametrize("mode", [cx.MODE_SHRED, cx.MODE_PRIMITIVE])
+def test_output_slab_rerun(engine, mode):
+    """A consensus longer than the tight output slab (kErrOut) is re-run with
+    full caps, by ccsx_gpu_run and inside ccsx_gpu_collect; a 64-byte tight
+    slab forces it for every ZMW but the tiny one."""
+    zs = [synth(6100 + h, 1500, 6) for h in range(4)] + [cx.prepare([b"ACGTACGTAC"] * 5)]
+    want, _, _ = batch(zs, mode, 5)
+    engine.set_tight_out(64)
+    try:
+        before = engine.rerun_count()
+        _check(engine, zs, mode)
+        assert engine.rerun_count() - before >= 4
+        s = engine.submit(zs, mode)
+        got = engine.collect(s)
+        assert [g for g, _, _ in got] == want and all(st == 0 for _, st, _ in got)
+    finally:
+        engine.set_tight_out(0)
+
+
 def test_tight_caps_fail_loudly_without_rerun(engine):
     """stage/launch/fetch (no re-run) reports the capacity status."""
     zs = [synth(h, 3000, 6) for h in range(2)]
