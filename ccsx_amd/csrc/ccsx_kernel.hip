@@ -294,40 +294,6 @@ __device__ __forceinline__ bool win_has(uint32_t c0, uint32_t nc, int32_t off)
     return (uint32_t)off >= c0 * kWinChunk && (uint32_t)off + 136u <= (c0 + nc) * kWinChunk;
 }
 
-// lane's 16-bit window of the read for a row at band offset `off`: the codes
-// of positions P .. P + 7, P = (off + 2 lane) & ~3 -- bytes (off + 2 lane) >> 2
-// and the next, from the LDS buffer, or the window / HBM on the HBM-read
-// instance (`inwin`: the wave may trust the window for this row).  The
-// lane's cells t = 2 lane, 2 lane + 1 of a row at offset off + d (0 <= d <= 3)
-// are win_codes(window, off, d).
-__device__ __forceinline__ uint32_t rd_win16(const Z &z, int32_t off, bool inwin)
-{
-    const uint32_t b = ((uint32_t)off + 2u * lane_id()) >> 2;
-#ifdef CCSX_RD_ALIGN
-    // the aligned dwords holding bytes b, b + 1, funnel-shifted (no unaligned
-    // 16-bit LDS access)
-    const uint32_t w = b >> 2, sh = (b & 3u) * 8u;
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(z.rd);
-    if (z.hbm && inwin) {
-        const uint32_t *win = reinterpret_cast<const uint32_t *>(z.win);
-        constexpr uint32_t wm = kRdWinBytes / 4 - 1;
-        return __builtin_amdgcn_alignbit(win[(w + 1) & wm], win[w & wm], sh);
-    }
-    return __builtin_amdgcn_alignbit(src[w + 1], src[w], sh);
-#else
-    if (!z.hbm) return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
-    if (inwin) return (uint32_t)z.win[b & kWinBytesMask] | (uint32_t)z.win[(b + 1) & kWinBytesMask] << 8;
-    return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
-#endif
-}
-
-// the codes of read positions off + d + 2 lane (bits 0-1) and the next (bits
-// 2-3) from the window rd_win16(z, off) loaded
-__device__ __forceinline__ uint32_t win_codes(uint32_t win, int32_t off, int32_t d)
-{
-    return win >> ((((uint32_t)off + 2u * lane_id()) & 3u) * 2u + 2u * (uint32_t)d);
-}
-
 // ----------------------------------------------------------------------------
 // push: stage read k (ASCII in HBM) into LDS as 2-bit codes, four per byte
 // (word w = positions 16 w .. 16 w + 15): 4,096 bases in 1 KiB, so the solo
@@ -364,6 +330,33 @@ constexpr int kLdsOffRing = kLdsDiag + (kHelpers ? 32 : 0);  // 64: band offset 
 constexpr int kLdsJob = kLdsOffRing + (kHelpers ? 64 : 0);   // 16: DP job / results
 constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
 
+
+// lane's 16-bit window of the read for a row at band offset `off`: the codes
+// of positions P .. P + 7, P = (off + 2 lane) & ~3 -- bytes (off + 2 lane) >> 2
+// and the next, from the LDS buffer, or the window / HBM on the HBM-read
+// instance (`inwin`: the wave may trust the window for this row).  The
+// lane's cells t = 2 lane, 2 lane + 1 of a row at offset off + d (0 <= d <= 3)
+// are win_codes(window, off, d).  The LDS buffer and the window both start
+// at word kLdsFixed of the dynamic LDS, which starts at address 0 (the
+// kernel declares no static __shared__): read through an LDS pointer of that
+// constant address, the buffer's base folds into the ds_read's offset field
+// (through z.rd the compiler kept a per-row `v_add 0` for the base).
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+__device__ __forceinline__ uint32_t rd_win16(const Z &z, int32_t off, bool inwin)
+{
+    const uint32_t b = ((uint32_t)off + 2u * lane_id()) >> 2;
+    const lds_u8 *lb = (const lds_u8 *)(uintptr_t)(kLdsFixed * 4);
+    if (!z.hbm) return (uint32_t)lb[b] | (uint32_t)lb[b + 1] << 8;
+    if (inwin) return (uint32_t)lb[b & kWinBytesMask] | (uint32_t)lb[(b + 1) & kWinBytesMask] << 8;
+    return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
+}
+
+// the codes of read positions off + d + 2 lane (bits 0-1) and the next (bits
+// 2-3) from the window rd_win16(z, off) loaded
+__device__ __forceinline__ uint32_t win_codes(uint32_t win, int32_t off, int32_t d)
+{
+    return win >> ((((uint32_t)off + 2u * lane_id()) & 3u) * 2u + 2u * (uint32_t)d);
+}
 
 // per lane: row r0+lane's info and first four predecessors
 struct RowPre {
@@ -1009,7 +1002,7 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
 // predecessor / D beat M, per cell; X = H' + 2 t; Pex = the insertion scan's
 // exclusive prefix max.  maybe_wide: the row may have more than 63
 // predecessors (its slots also go to the wide slot records).
-template <bool FULL>
+template <bool FULL, bool TRACK_OFF = true>
 __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, int32_t &bOff,
                                            const __amdgpu_buffer_rsrc_t &rc, uint32_t r, uint32_t m, int32_t lim,
                                            int32_t off, uint32_t np, bool maybe_wide, const PredAcc &A, const LaneK &c,
@@ -1044,11 +1037,13 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
         if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
     }
     // rows come in order: the first maximum is the earliest (min row, min cell)
-    if (e0 > bE) bE = e0, bKey = r * 2, bOff = off;
-    if (e1 > bE) bE = e1, bKey = r * 2 + 1, bOff = off;
+    // (TRACK_OFF false: the caller looks the winner's band offset up in the
+    // row meta afterwards -- two VALU per row fewer)
+    if (e0 > bE) bE = e0, bKey = r * 2, bOff = TRACK_OFF ? off : bOff;
+    if (e1 > bE) bE = e1, bKey = r * 2 + 1, bOff = TRACK_OFF ? off : bOff;
     // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
-    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, r * 256u + (((uint32_t)lane * 4u + tb_rot(r)) & 255u), 0,
-                                          0);
+    // (the row's base as the store's scalar offset)
+    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, ((uint32_t)lane * 4u + tb_rot(r)) & 255u, r * 256u, 0);
 }
 
 // helper wave: everything after the predecessor terms of row r (SPEC.md
@@ -1272,8 +1267,7 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
 // ----------------------------------------------------------------------------
 struct SolB {
     int32_t bE;       // best free-end value of this lane's cells
-    uint32_t bKey;    // its row * 2 + cell
-    int32_t bOff;     // its row's band offset
+    uint32_t bKey;    // its row * 2 + cell (the row's band offset: row meta)
     __amdgpu_buffer_rsrc_t rc;  // cell records of this DP (R rows x 256 B)
 };
 
@@ -1288,7 +1282,12 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
     const uint32_t np = info >> 8;
     const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
     const int32_t sh = coff - S.pOff;
+#ifdef CCSX_FAST_ARITH
+    // (integer arithmetic only: a bool of the band test lowers to lane masks)
+    const uint32_t fast = (uint32_t)(S.fmask >> li) & (3u >> min((uint32_t)sh, 2u)) & 1u;
+#else
     const uint32_t fast = (uint32_t)(S.fmask >> li) & ((uint32_t)sh <= 1u ? 1u : 0u);
+#endif
     // everything after the predecessor terms: the recurrence (dpA_row's
     // tail) and the decision bits (dpB_tail's) from the same values;
     // instantiated on both sides of the fast / cold branch, so a fast row's
@@ -1343,7 +1342,8 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         S.pArg = off + 127 - (key & 127);
         // decision bits, free-end candidates, record (only a cold row can
         // have more than 63 predecessors)
-        row_record<FULL>(z, B.bE, B.bKey, B.bOff, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0,
+        int32_t no_off = 0;
+        row_record<FULL, false>(z, B.bE, B.bKey, no_off, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0,
                          X1, Pex);
     };
     if (__builtin_expect(fast, 1)) {
@@ -1430,7 +1430,7 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
     S.W.nxt = S.W.cur;
     SolB B;
-    B.bE = INT32_MIN, B.bKey = 0, B.bOff = 0;
+    B.bE = INT32_MIN, B.bKey = 0;
     B.rc = brsrc(z.ws + z.L.codes, z.R * 256u);
     const uint32_t nblk = dp_nblk(z.R);
     for (uint32_t b = 0; b < nblk && !z.status; ++b) {
@@ -1449,10 +1449,17 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     const uint32_t rsel = B.bE == best ? B.bKey >> 1 : 0x7FFFFFFFu;
     const int32_t rmin = wave_min((int32_t)rsel);
     const bool mine = B.bE == best && (B.bKey >> 1) == (uint32_t)rmin;
-    const int32_t jsel = mine ? B.bOff + 2 * lane + (int32_t)(B.bKey & 1u) : INT32_MAX;
+    wsync();  // records and row meta in HBM before the traceback's DMA (and the load below) reads them
+    // the winning row's band offset from the row meta (L1 bypassed: this
+    // wave's stores went to L2)
+    int32_t boff = 0;
+    if (best != INT32_MIN) {
+        const auto rm = brsrc(reinterpret_cast<uint32_t *>(z.ws + z.L.rmeta), z.R * 4u);
+        boff = (int32_t)(uni(__builtin_amdgcn_raw_buffer_load_b32(rm, (uint32_t)rmin * 4u, 0, 1)) & 0x7FFFFFFFu);
+    }
+    const int32_t jsel = mine ? boff + 2 * lane + (int32_t)(B.bKey & 1u) : INT32_MAX;
     er_out = best == INT32_MIN ? 0xFFFFFFFFu : (uint32_t)rmin;
     ej_out = (uint32_t)wave_min(jsel);
-    wsync();  // records and row meta in HBM before the traceback's DMA reads them
     z.cells += (unsigned long long)z.R * (m < (uint32_t)kW ? m : (uint32_t)kW);
 }
 
