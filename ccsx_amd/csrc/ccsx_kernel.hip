@@ -1039,8 +1039,16 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
     // rows come in order: the first maximum is the earliest (min row, min cell)
     // (TRACK_OFF false: the caller looks the winner's band offset up in the
     // row meta afterwards -- two VALU per row fewer)
-    if (e0 > bE) bE = e0, bKey = r * 2, bOff = TRACK_OFF ? off : bOff;
-    if (e1 > bE) bE = e1, bKey = r * 2 + 1, bOff = TRACK_OFF ? off : bOff;
+    if (!TRACK_OFF) {
+        // the lane's two cells first (cell 1 only if strictly better), then
+        // against the best so far: the same first maximum
+        const bool c1 = e1 > e0;
+        const int32_t e01 = c1 ? e1 : e0;
+        if (e01 > bE) bE = e01, bKey = r * 2 + (c1 ? 1u : 0u);
+    } else {
+        if (e0 > bE) bE = e0, bKey = r * 2, bOff = TRACK_OFF ? off : bOff;
+        if (e1 > bE) bE = e1, bKey = r * 2 + 1, bOff = TRACK_OFF ? off : bOff;
+    }
     // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
     // (the row's base as the store's scalar offset)
     __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, ((uint32_t)lane * 4u + tb_rot(r)) & 255u, r * 256u, 0);
@@ -1282,12 +1290,9 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
     const uint32_t np = info >> 8;
     const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
     const int32_t sh = coff - S.pOff;
-#ifdef CCSX_FAST_ARITH
-    // (integer arithmetic only: a bool of the band test lowers to lane masks)
+    // integer arithmetic only (a bool of the band test lowered to lane-mask
+    // selects and a vcc branch: 0.7-0.8 % on D / E16k, A/B r04za)
     const uint32_t fast = (uint32_t)(S.fmask >> li) & (3u >> min((uint32_t)sh, 2u)) & 1u;
-#else
-    const uint32_t fast = (uint32_t)(S.fmask >> li) & ((uint32_t)sh <= 1u ? 1u : 0u);
-#endif
     // everything after the predecessor terms: the recurrence (dpA_row's
     // tail) and the decision bits (dpB_tail's) from the same values;
     // instantiated on both sides of the fast / cold branch, so a fast row's
