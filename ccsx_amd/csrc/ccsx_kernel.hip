@@ -346,6 +346,10 @@ __device__ __forceinline__ uint32_t rd_win16(const Z &z, int32_t off, bool inwin
 {
     const uint32_t b = ((uint32_t)off + 2u * lane_id()) >> 2;
     const lds_u8 *lb = (const lds_u8 *)(uintptr_t)(kLdsFixed * 4);
+#ifdef CCSX_RD_U16
+    typedef __attribute__((address_space(3))) const uint16_t __attribute__((aligned(1))) lds_u16u;
+    if (!z.hbm) return *(const lds_u16u *)(lb + b);
+#endif
     if (!z.hbm) return (uint32_t)lb[b] | (uint32_t)lb[b + 1] << 8;
     if (inwin) return (uint32_t)lb[b & kWinBytesMask] | (uint32_t)lb[(b + 1) & kWinBytesMask] << 8;
     return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
@@ -796,7 +800,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
     const int32_t sh = coff - S.pOff;
     // (an integer test keeps the branch scalar: a bool of && lowers to a lane mask)
-    const uint32_t fast = (uint32_t)(S.fmask >> li) & ((uint32_t)sh <= 1u ? 1u : 0u);
+    const uint32_t fast = (uint32_t)(S.fmask >> li) & (3u >> min((uint32_t)sh, 2u)) & 1u;  // (as dpS_row)
 #ifdef CCSX_DP_STAMPS
     unsigned long long ts0, ts1, ts2, ts3;
     int ckind = 0;
@@ -804,6 +808,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
 #endif
     // everything after the predecessor terms; instantiated on both sides of
     // the fast / cold branch so a fast row meets no further branch
+    int32_t row_key = 0;  // the row's key (readlane of the max-scan)
     auto tail = [&](int32_t off, uint32_t qp, int32_t Mh0, int32_t Mh1, int32_t Dv0, int32_t Dv1,
                     bool cold) __attribute__((always_inline)) {
         // the next row's read window, a row ahead of its use (its offset lies
@@ -839,10 +844,8 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
-        // (inline asm measured 0.6 % faster than the compiler's writelane
-        // intrinsic here: it keeps vOff / vKey out of the scheduler's way)
-        S.vOff = writelane(S.vOff, off, li);
-        S.vKey = writelane(S.vKey, key, li);
+        // (the offset / key vectors after the fast / cold join, below)
+        row_key = key;
         if (cold && (info & kInfoSpill)) {
             // a successor lies beyond the ring: keep this row in HBM
             const uint32_t sl = S.nspill++;
@@ -923,6 +926,11 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
                                     : win_codes(rd_win16(z, off, z.hbm && win_has(z.wa, 2, off)), off, 0);
         tail(off, qp, Mh0, Mh1, Dv0, Dv1, true);
     }
+    // (inline asm measured 0.6 % faster than the compiler's writelane
+    // intrinsic: it keeps vOff / vKey out of the scheduler's way; after the
+    // join, one pair instead of a pair plus two register copies per branch)
+    S.vOff = writelane(S.vOff, S.pOff, li);
+    S.vKey = writelane(S.vKey, row_key, li);
 }
 
 // wave 0: rows [r0, r0 + kBlkAB)
@@ -1297,6 +1305,7 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
     // tail) and the decision bits (dpB_tail's) from the same values;
     // instantiated on both sides of the fast / cold branch, so a fast row's
     // tags are constants and it meets no further branch
+    int32_t row_key = 0;  // the row's key (readlane of the max-scan), for the offset / key vectors after the branch
     auto tail = [&](int32_t off, uint32_t qp, const PredAcc &A, bool cold) __attribute__((always_inline)) {
         // the next row's read window, a row ahead of its use
         S.qn = rd_win16(z, off, z.hbm && win_has(z.wa, 2, off));
@@ -1328,8 +1337,7 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
         row[0] = make_int2(nH0, nH1);
         row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
-        S.vOff = writelane(S.vOff, off, li);
-        S.vKey = writelane(S.vKey, key, li);
+        row_key = key;
         if (cold && (info & kInfoSpill)) {
             // a successor lies beyond the ring: keep this row in HBM
             const uint32_t sl = S.nspill++;
@@ -1379,6 +1387,10 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
                                     : win_codes(rd_win16(z, off, z.hbm && win_has(z.wa, 2, off)), off, 0);
         tail(off, qp, A, true);
     }
+    // one writelane pair after the fast / cold join (inside each branch the
+    // tied operands cost two register copies per row: E16k -0.7 %, r04zb)
+    S.vOff = writelane(S.vOff, S.pOff, li);
+    S.vKey = writelane(S.vKey, row_key, li);
 }
 
 // rows [r0, r0 + kBlkAB) and, per 16-row group, the row meta words {band
