@@ -340,16 +340,14 @@ constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibb
 // at word kLdsFixed of the dynamic LDS, which starts at address 0 (the
 // kernel declares no static __shared__): read through an LDS pointer of that
 // constant address, the buffer's base folds into the ds_read's offset field
-// (through z.rd the compiler kept a per-row `v_add 0` for the base).
+// (through z.rd the compiler kept a per-row `v_add 0` for the base).  The two
+// bytes as two ds_read_u8: one unaligned ds_read_u16 measured 0.4 % slower
+// (r04zd).
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;
 __device__ __forceinline__ uint32_t rd_win16(const Z &z, int32_t off, bool inwin)
 {
     const uint32_t b = ((uint32_t)off + 2u * lane_id()) >> 2;
     const lds_u8 *lb = (const lds_u8 *)(uintptr_t)(kLdsFixed * 4);
-#ifdef CCSX_RD_U16
-    typedef __attribute__((address_space(3))) const uint16_t __attribute__((aligned(1))) lds_u16u;
-    if (!z.hbm) return *(const lds_u16u *)(lb + b);
-#endif
     if (!z.hbm) return (uint32_t)lb[b] | (uint32_t)lb[b + 1] << 8;
     if (inwin) return (uint32_t)lb[b & kWinBytesMask] | (uint32_t)lb[(b + 1) & kWinBytesMask] << 8;
     return (uint32_t)z.rd[b] | (uint32_t)z.rd[b + 1] << 8;
@@ -1365,17 +1363,22 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         PredAcc A;
         A.ms0 = A.ms1 = A.ds0 = A.ds1 = 1u;
         int32_t a0, b0, a1, b1;
+        // the tail instantiated per band move: no join of the predecessor
+        // terms (whose register copies cost ~5 VALU per row; E16k -0.4 %, r04zd)
         if (sh == 0) {
             A.Mh0 = wave_shr1(kNegH, S.H1), A.Mh1 = S.H0;
             a0 = S.H0 + (kO + kE), b0 = S.D0 + kE, a1 = S.H1 + (kO + kE), b1 = S.D1 + kE;
+            A.Dv0 = max(a0, b0), A.Dv1 = max(a1, b1);
+            A.dx0 = b0 > a0 ? 4u : 0u, A.dx1 = b1 > a1 ? 4u : 0u;
+            tail(coff, win_codes(S.qn, S.pOff, 0), A, false);
         } else {
             A.Mh0 = S.H0, A.Mh1 = S.H1;
             a0 = S.H1 + (kO + kE), b0 = S.D1 + kE;
             a1 = wave_shl1(kNegH, S.H0) + (kO + kE), b1 = wave_shl1(kNeg, S.D0) + kE;
+            A.Dv0 = max(a0, b0), A.Dv1 = max(a1, b1);
+            A.dx0 = b0 > a0 ? 4u : 0u, A.dx1 = b1 > a1 ? 4u : 0u;
+            tail(coff, win_codes(S.qn, S.pOff, 1), A, false);
         }
-        A.Dv0 = max(a0, b0), A.Dv1 = max(a1, b1);
-        A.dx0 = b0 > a0 ? 4u : 0u, A.dx1 = b1 > a1 ? 4u : 0u;
-        tail(coff, win_codes(S.qn, S.pOff, sh), A, false);
     } else {
         PredAcc A;
         int32_t off;
