@@ -85,7 +85,11 @@ for f in ("kt_kernel_stats.csv",):
     p = glob.glob(os.path.join(src, "kt", "*" + f))
     if p:
         open(os.path.join(ROOT, "profiles", f"{tag}_{f}"), "w").write(open(p[0]).read())
-cfg = sys.argv[2] if len(sys.argv) > 2 else "B"  # the bench config profiled (traffic.json key)
+# the bench config profiled (traffic.json key): the second argument, else the
+# tag's suffix (r04ze_E16384 -> E16384); never a silent default
+cfg = sys.argv[2] if len(sys.argv) > 2 else tag.rsplit("_", 1)[-1]
+if cfg not in ("B", "C", "D", "E", "H", "HP", "E16384"):
+    raise SystemExit(f"traffic.json key: pass the config as the second argument (tag suffix {cfg!r} is not one)")
 tj = os.path.join(ROOT, "profiles", "traffic.json")
 t = json.load(open(tj)) if os.path.exists(tj) else {}
 t[cfg] = {"bytes_per_launch": fetch_b + write_b, "fetch_bytes": fetch_b, "write_bytes": write_b,
