@@ -133,6 +133,7 @@ struct Chunk {
     ~Chunk() { release_arena(); }
     std::atomic<size_t> pending{0};  // batches not yet back from a device
     double t_read0 = 0, t_read1 = 0;  // CCSX_TIMING: when step 0's reader read it
+    bool last_input = false;           // the input ended inside this chunk
 };
 
 struct Batch {
@@ -517,6 +518,10 @@ int main(int argc, char **argv)
     // r03o)
     uint32_t batches_per_ctx = 1;
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    // the chunk the input ends in: batches per context (the run ends on its
+    // slowest batch; smaller ones let the contexts end together)
+    uint32_t last_batches_per_ctx = 1;
+    if (const char *e = getenv("CCSX_LAST_BATCHES")) last_batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     const auto tstart = std::chrono::steady_clock::now();
     auto now_ms = [tstart]() {
@@ -685,7 +690,7 @@ int main(int argc, char **argv)
             std::vector<Zmw> &zs = ch->zs;
             ch->t_read0 = now_ms();
             ccsx_ingest::ZmwRef zr;
-            int l;
+            int l = 0;
             while (!fatal && (l = rd->next(zr)) >= 0) {
                 if (l < min_fulllen_count + 2) continue;
                 const uint64_t total = zr.total();
@@ -700,6 +705,7 @@ int main(int argc, char **argv)
                 }
             }
             ch->t_read1 = now_ms();
+            ch->last_input = l < 0;
             // kt_pipeline stops on an empty chunk (main.c:694-697); a chunk
             // cut short by -1 (end of input or an invalid name) is processed
             // and the next read goes on, as the reference's next step 0 does
@@ -830,7 +836,7 @@ int main(int argc, char **argv)
         std::vector<uint64_t> cost(n);
         for (uint32_t i = 0; i < n; ++i) cost[i] = ccsx_zmw_cost(zs[i].seg_len.data(), (uint32_t)zs[i].seg_len.size());
         std::vector<uint32_t> order(n), bounds(n + 1);
-        uint32_t nparts = (uint32_t)nctx * batches_per_ctx;
+        uint32_t nparts = (uint32_t)nctx * (ch->last_input ? std::max(batches_per_ctx, last_batches_per_ctx) : batches_per_ctx);
         if (async) {
             uint64_t bytes = 0;
             for (uint32_t i = 0; i < n; ++i) {
