@@ -96,6 +96,25 @@ struct MmapSource : ByteSource {
     std::shared_ptr<Block> b;
     std::thread toucher;
     std::atomic<bool> stop{false};
+    std::atomic<size_t> touched{0};  // the toucher is past this offset
+    std::mutex rel_m;
+    size_t released = 0;  // [0, released) unmapped
+    // the caller reads no byte below `upto` any more: unmap those pages (the
+    // teardown of a 65 GB mapping otherwise falls on the process exit), never
+    // above what the toucher has passed
+    void release(const char *upto)
+    {
+        std::lock_guard<std::mutex> g(rel_m);
+        if (!b->map || !upto) return;
+        const char *base = static_cast<const char *>(b->map);
+        if (upto <= base) return;
+        size_t hi = std::min<size_t>((size_t)(upto - base), touched.load());
+        hi &= ~size_t(4095);
+        if (hi > released) {
+            munmap(const_cast<char *>(base) + released, hi - released);
+            released = hi;
+        }
+    }
     MmapSource(int fd, size_t size)
     {
         b = std::make_shared<Block>();
@@ -111,7 +130,11 @@ struct MmapSource : ByteSource {
         toucher = std::thread([this, m, size] {
             volatile const char *p = static_cast<const char *>(m);
             char sink = 0;
-            for (size_t o = 0; o < size && !stop; o += 4096) sink ^= p[o];
+            for (size_t o = 0; o < size && !stop; o += 4096) {
+                sink ^= p[o];
+                if ((o & ((2u << 20) - 1)) == 0) touched.store(o);
+            }
+            touched.store(size);
             (void)sink;
         });
     }
@@ -678,7 +701,11 @@ int split3(const std::string &name, std::string f[3], std::string &shown)
 // ---------------------------------------------------------------- grouping
 class Grouper : public ZmwSource {
 public:
-    explicit Grouper(std::unique_ptr<RecordReader> rr) : rr_(std::move(rr)) {}
+    Grouper(std::unique_ptr<RecordReader> rr, MmapSource *mm) : rr_(std::move(rr)), mm_(mm) {}
+    void release(const char *upto) override
+    {
+        if (mm_) mm_->release(upto);
+    }
     // (a negative record value ends this call only: the reference's next
     // step 0 calls kseq_zmw_read again and reads on, e.g. after a bad FASTQ
     // record)
@@ -723,6 +750,7 @@ public:
 
 private:
     std::unique_ptr<RecordReader> rr_;
+    MmapSource *mm_;  // the whole-file mapping the records point into (owned by rr_), or null
     bool have_last_ = false;
     std::string last_movie_, last_hole_;
     Rec last_rec_;
@@ -741,6 +769,7 @@ std::unique_ptr<ZmwSource> ZmwSource::open(const char *path, bool is_bam, int nt
     const char *e = getenv("CCSX_INGEST_BLOCK");
     const size_t block = e ? (size_t)std::max<long>(1, atol(e)) : (32u << 20);
     std::unique_ptr<ByteSource> src;
+    MmapSource *mm = nullptr;
     // stdin redirected from a regular file, not read yet: the file's own
     // path below (mmap, parallel BGZF, gzread), else a gzread stream
     bool stdin_stream = false;
@@ -775,7 +804,7 @@ std::unique_ptr<ZmwSource> ZmwSource::open(const char *path, bool is_bam, int nt
         } else {
             struct stat st;
             if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0 && !getenv("CCSX_INGEST_BLOCK"))
-                src.reset(new MmapSource(fd, (size_t)st.st_size));
+                src.reset(mm = new MmapSource(fd, (size_t)st.st_size));
             else
                 src.reset(new FdSource(fd));
         }
@@ -784,7 +813,7 @@ std::unique_ptr<ZmwSource> ZmwSource::open(const char *path, bool is_bam, int nt
     std::unique_ptr<RecordReader> rr;
     if (is_bam) rr.reset(new BamReader(std::move(src)));
     else rr.reset(new FxReader(std::move(src)));
-    return std::unique_ptr<ZmwSource>(new Grouper(std::move(rr)));
+    return std::unique_ptr<ZmwSource>(new Grouper(std::move(rr), mm));
 }
 
 }  // namespace ccsx_ingest

@@ -61,6 +61,9 @@ public:
     // count), or -1 at the end of input or after an invalid record name
     // ("invalid zmw name :<name>" on stderr; the next call reads on)
     virtual int next(ZmwRef &z) = 0;
+    // the caller reads no record byte below `upto` any more (records of
+    // earlier ZMWs): a mapped input may unmap those pages
+    virtual void release(const char *upto) { (void)upto; }
 };
 
 }  // namespace ccsx_ingest

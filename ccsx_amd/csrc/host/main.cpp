@@ -134,6 +134,7 @@ struct Chunk {
     std::atomic<size_t> pending{0};  // batches not yet back from a device
     double t_read0 = 0, t_read1 = 0;  // CCSX_TIMING: when step 0's reader read it
     bool last_input = false;           // the input ended inside this chunk
+    const char *input_hi = nullptr;    // end of the last record read into it (ZmwSource::release)
 };
 
 struct Batch {
@@ -518,6 +519,11 @@ int main(int argc, char **argv)
     // r03o)
     uint32_t batches_per_ctx = 1;
     if (const char *e = getenv("CCSX_CTX_BATCHES")) batches_per_ctx = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    // consumed input pages unmapped as chunks are prepared (CCSX_INPUT_RELEASE=0: at the exit)
+    const bool input_release = !(getenv("CCSX_INPUT_RELEASE") && atoi(getenv("CCSX_INPUT_RELEASE")) == 0);
+    // a context with no more work releases its memory while the others run
+    // (CCSX_EARLY_CLOSE=0: the exit releases everything)
+    const bool early_close = !(getenv("CCSX_EARLY_CLOSE") && atoi(getenv("CCSX_EARLY_CLOSE")) == 0);
     // the chunk the input ends in: batches per context (the run ends on its
     // slowest batch; smaller ones let the contexts end together)
     uint32_t last_batches_per_ctx = 1;
@@ -665,7 +671,7 @@ int main(int argc, char **argv)
         // The output waits for the work, not for the release (work_done)
         const bool last = workers_busy.fetch_sub(1) == 1;
         work_done(w);
-        if (!fatal && !last) {
+        if (!fatal && !last && early_close) {
             ccsx_gpu_close(ctx[w]);
             ctx[w] = nullptr;
         }
@@ -692,6 +698,7 @@ int main(int argc, char **argv)
             ccsx_ingest::ZmwRef zr;
             int l = 0;
             while (!fatal && (l = rd->next(zr)) >= 0) {
+                for (const auto &rc : zr.recs) ch->input_hi = std::max(ch->input_hi, rc.seq + rc.span);
                 if (l < min_fulllen_count + 2) continue;
                 const uint64_t total = zr.total();
                 if (total > (uint64_t)max_subread_len || total < (uint64_t)min_subread_len) continue;
@@ -829,6 +836,9 @@ int main(int argc, char **argv)
         const size_t id = ch->id;
         const double t0 = ch->t_read0, t1 = ch->t_read1;
         prepare_chunk(*ch, nthreads, verbose);
+        // the chunk's bases are in its arena: its input pages go (a mapped
+        // file is unmapped behind the reader instead of all at the exit)
+        if (input_release) rd->release(ch->input_hi);
         await_open();
         // cost-balanced micro-batches: cost ranks dealt round-robin, each
         // batch longest first (dispatch.cpp)
