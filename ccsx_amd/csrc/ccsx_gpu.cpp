@@ -175,6 +175,7 @@ struct DevBuf {
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t evp[2] = {nullptr, nullptr};  // piecewise staging: the copy out of each half of h_seq
     size_t nz = 0;
     uint32_t lds_read_words = 0, lds_nmax = 0, lds_extra = 0;
     int32_t cfg = ccsx::kCfgLatency;   // kernel configuration of the staged slice
@@ -197,6 +198,8 @@ struct Slot {
         for (DevBuf *b : bufs) b->release();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        for (hipEvent_t &e : evp)
+            if (e) (void)hipEventDestroy(e), e = nullptr;
         if (stream) (void)hipStreamDestroy(stream);
         ev0 = ev1 = nullptr;
         stream = nullptr;
@@ -226,6 +229,7 @@ struct ccsx_ctx {
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
     uint32_t tight_out = 0;            // test hook: override the tight output slab
+    uint64_t stage_piece = 0;          // test hook: piecewise staging's half size (0: kStagePiece)
     int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
     bool shred_caps = false;           // tight caps sized for shredding windows (ccsx_gpu_run, shredded mode)
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
@@ -280,6 +284,8 @@ int ccsx_gpu_open(int device, ccsx_ctx **out)
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreate(&s.ev0);
         if (e == hipSuccess) e = hipEventCreate(&s.ev1);
+        for (hipEvent_t &p : s.evp)
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&p, hipEventDisableTiming);
     }
     if (e == hipSuccess) {
         int n = 0;
@@ -341,6 +347,8 @@ const char *ccsx_gpu_status_str(int32_t s)
 // context's two batches: ~1 GB of subreads) without re-pinning; grown on
 // demand beyond it.  INTEGRATION.md lists the host-memory footprint.
 constexpr size_t kPinnedSeqFloor = 512ull << 20, kPinnedOutFloor = 128ull << 20;
+// piecewise staging of a CLI context's subreads: two pinned halves of this
+constexpr size_t kStagePiece = 64ull << 20;
 
 // LDS read buffer limits of the LDS kernel instance: reads up to 100 kb
 // (25 KiB of 2-bit codes) and 4,096 segments; beyond
@@ -506,18 +514,32 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
     if (bp_w) HIPCHK(c, s.d_bp.reserve(bp_w * 4));
     const auto tb = std::chrono::steady_clock::now();
     // host staging of the sequence arena and segment tables
-    HIPCHK(c, s.h_seq.reserve(seq_b, c->prealloc ? kPinnedSeqFloor / c->mem_share : 0));
-    uint8_t *hseq = s.h_seq.p;
     s.hoff.resize(nseg);
     s.hlen.resize(nseg);
-    // the packing is a memory copy of the whole slice's subreads (1.8 GB for
-    // a 10k-ZMW config-E slice, ~100 ms on one thread): split over threads,
-    // since the slice's kernel cannot start before it is done (16,384-ZMW
-    // e2e line 17.3k -> 19.2k ZMWs/s, r03y).  Contexts sharing a device (the
-    // CLI's two per GPU) stage while the other's kernels run and keep to one
-    // thread, leaving the CPUs to the host pipeline's preparation.
-    auto pack = [&](size_t i0, size_t i1) {
-        for (size_t i = i0; i < i1; ++i) {
+    const size_t nthr = c->mem_share > 1 ? 1 : std::min<size_t>(std::min<size_t>(8, nz), std::max<uint64_t>(1, seq_b >> 27));
+    const size_t piece = c->stage_piece ? (size_t)c->stage_piece : kStagePiece;
+    if (c->prealloc && nthr <= 1 && seq_b > 2 * piece) {
+        // a context sharing its device (the CLI's): packed on this thread in
+        // pieces through two pinned halves of kStagePiece, each copied while
+        // the next is packed -- 128 MiB pinned per slot instead of the whole
+        // slice (~1.1 GB for 8,192 config-E ZMWs), which the process exit or
+        // ccsx_gpu_close otherwise pays to unpin
+        HIPCHK(c, s.h_seq.reserve(2 * piece, 0, true));
+        uint8_t *buf[2] = {s.h_seq.p, s.h_seq.p + piece};
+        bool used[2] = {false, false};
+        int pb = 0;
+        size_t ps = 0, fill = 0;  // the piece's slice offset and its bytes
+        auto flush = [&]() -> hipError_t {
+            hipError_t e = hipMemcpyAsync(s.d_seq.as<uint8_t>() + ps, buf[pb], fill, hipMemcpyHostToDevice, s.stream);
+            if (e == hipSuccess) e = hipEventRecord(s.evp[pb], s.stream);
+            used[pb] = true;
+            ps += fill, fill = 0;
+            pb ^= 1;
+            // the other half's copy has to be done before it is refilled
+            if (e == hipSuccess && used[pb]) e = hipEventSynchronize(s.evp[pb]);
+            return e;
+        };
+        for (size_t i = 0; i < nz; ++i) {
             const ccsx_zmw_in &zi = z[i];
             const ccsx::ZmwDesc &d = s.desc[i];
             uint64_t hi = 0;
@@ -526,19 +548,47 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
                 s.hlen[d.seg0 + k] = zi.seg_len[k];
                 hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
             }
-            if (hi) memcpy(hseq + d.seq_off, zi.seqs, hi);
+            // (d.seq_off == ps + fill: ZMWs are packed back to back)
+            for (uint64_t done = 0; done < hi;) {
+                const size_t n = (size_t)std::min<uint64_t>(hi - done, piece - fill);
+                memcpy(buf[pb] + fill, zi.seqs + done, n);
+                fill += n, done += n;
+                if (fill == piece) HIPCHK(c, flush());
+            }
         }
-    };
-    const size_t nthr = c->mem_share > 1 ? 1 : std::min<size_t>(std::min<size_t>(8, nz), std::max<uint64_t>(1, seq_b >> 27));
-    if (nthr <= 1) {
-        pack(0, nz);
+        if (fill) HIPCHK(c, flush());
     } else {
-        std::vector<std::thread> th;
-        for (size_t t = 1; t < nthr; ++t) th.emplace_back(pack, nz * t / nthr, nz * (t + 1) / nthr);
-        pack(0, nz / nthr);
-        for (auto &x : th) x.join();
+        HIPCHK(c, s.h_seq.reserve(seq_b, c->prealloc ? kPinnedSeqFloor / c->mem_share : 0));
+        uint8_t *hseq = s.h_seq.p;
+        // the packing is a memory copy of the whole slice's subreads (1.8 GB for
+        // a 10k-ZMW config-E slice, ~100 ms on one thread): split over threads,
+        // since the slice's kernel cannot start before it is done (16,384-ZMW
+        // e2e line 17.3k -> 19.2k ZMWs/s, r03y).  Contexts sharing a device (the
+        // CLI's two per GPU) stage while the other's kernels run and keep to one
+        // thread, leaving the CPUs to the host pipeline's preparation.
+        auto pack = [&](size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; ++i) {
+                const ccsx_zmw_in &zi = z[i];
+                const ccsx::ZmwDesc &d = s.desc[i];
+                uint64_t hi = 0;
+                for (uint32_t k = 0; k < zi.nseg; ++k) {
+                    s.hoff[d.seg0 + k] = zi.seg_off[k];
+                    s.hlen[d.seg0 + k] = zi.seg_len[k];
+                    hi = std::max<uint64_t>(hi, uint64_t(zi.seg_off[k]) + zi.seg_len[k]);
+                }
+                if (hi) memcpy(hseq + d.seq_off, zi.seqs, hi);
+            }
+        };
+        if (nthr <= 1) {
+            pack(0, nz);
+        } else {
+            std::vector<std::thread> th;
+            for (size_t t = 1; t < nthr; ++t) th.emplace_back(pack, nz * t / nthr, nz * (t + 1) / nthr);
+            pack(0, nz / nthr);
+            for (auto &x : th) x.join();
+        }
+        HIPCHK(c, hipMemcpyAsync(s.d_seq.p, hseq, seq_b, hipMemcpyHostToDevice, s.stream));
     }
-    HIPCHK(c, hipMemcpyAsync(s.d_seq.p, hseq, seq_b, hipMemcpyHostToDevice, s.stream));
     HIPCHK(c, hipMemcpyAsync(s.d_soff.p, s.hoff.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, s.stream));
     HIPCHK(c, hipMemcpyAsync(s.d_slen.p, s.hlen.data(), size_t(nseg) * 4, hipMemcpyHostToDevice, s.stream));
     HIPCHK(c, hipMemcpyAsync(s.d_desc.p, s.desc.data(), nz * sizeof(ccsx::ZmwDesc), hipMemcpyHostToDevice, s.stream));
@@ -979,7 +1029,10 @@ int ccsx_gpu_reserve_staging(ccsx_ctx *c, uint64_t seq_bytes, uint64_t out_bytes
 {
     if (!c) return -1;
     HIPCHK(c, hipSetDevice(c->device));
-    // the slot the next submit takes; exact sizes (a later batch grows them)
+    // the slot the next submit takes; exact sizes (a later batch grows them).
+    // A context sharing its device stages subreads piecewise: two halves
+    if (c->prealloc && c->mem_share > 1)
+        seq_bytes = std::min<uint64_t>(seq_bytes, 2 * (c->stage_piece ? c->stage_piece : kStagePiece));
     for (int k = 0; k < 2; ++k) {
         if (c->tk[k].pending) continue;
         Slot &s = c->slot[k];
@@ -1141,6 +1194,13 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *c, uint32_t rows)
 {
     if (!c) return -1;
     c->tight_rows = rows;
+    return 0;
+}
+
+int ccsx_gpu_set_stage_piece(ccsx_ctx *c, uint64_t bytes)
+{
+    if (!c) return -1;
+    c->stage_piece = bytes;
     return 0;
 }
 

@@ -137,6 +137,11 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
 /* Test hook: tight output slab override in bytes (0 = default 2 x longest
  * segment + 1,024; a consensus beyond it re-runs the ZMW with full caps). */
 int ccsx_gpu_set_tight_out(ccsx_ctx *ctx, uint32_t bytes);
+/* Test hook: half size of the piecewise subread staging (0 = 64 MiB) that a
+ * preallocating context sharing its device (ccsx_gpu_set_prealloc,
+ * ccsx_gpu_set_mem_share > 1: the CLI's) uses for slices larger than two
+ * halves: 128 MiB pinned per slot instead of the whole slice. */
+int ccsx_gpu_set_stage_piece(ccsx_ctx *ctx, uint64_t bytes);
 /* Kernel configuration of the next slices: -1 (default) = by slice size (the
  * latency configuration 0 -- three waves, 8-row DP blocks, 32-row LDS ring --
  * when it keeps the whole slice resident; the solo configuration 3 -- one

@@ -166,6 +166,27 @@ def test_output_slab_rerun(engine, mode):
         engine.set_tight_out(0)
 
 
+def test_piecewise_staging():
+    """A preallocating context sharing its device (the CLI's) stages subreads
+    through two pinned halves; 4 KiB halves here, so pieces split ZMWs and
+    every copy waits on the one before last.  ccsx_gpu_run and submit /
+    collect both equal the oracle."""
+    zs = [synth(6300 + h, 2500, 6) for h in range(6)]
+    want, _, _ = batch(zs, cx.MODE_SHRED, 6)
+    e = cx.Engine(0)
+    try:
+        e.set_prealloc(True)
+        e.set_mem_share(2)
+        e.set_stage_piece(4096)
+        got = e.run(zs, cx.MODE_SHRED)
+        assert [g for g, _, _ in got] == want and all(st == 0 for _, st, _ in got)
+        s = e.submit(zs[:4])
+        got = e.collect(s)
+        assert [g for g, _, _ in got] == want[:4]
+    finally:
+        e.close()
+
+
 def test_tight_caps_fail_loudly_without_rerun(engine):
     """stage/launch/fetch (no re-run) reports the capacity status."""
     zs = [synth(h, 3000, 6) for h in range(2)]

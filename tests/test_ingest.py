@@ -25,8 +25,9 @@ def ingest_bench():
         os.makedirs(os.path.dirname(BENCH), exist_ok=True)
         subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-I",
                         os.path.join(ROOT, "ccsx_amd", "csrc", "host"), src, "-L", os.path.join(ROOT, "ccsx_amd"),
-                        "-lccsx_amd", "-lz", "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "ccsx_amd"), "-o", BENCH],
-                       check=True)
+                        "-lccsx_amd", "-lz", "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "ccsx_amd"), "-o",
+                        BENCH + f".{os.getpid()}"], check=True)
+        os.replace(BENCH + f".{os.getpid()}", BENCH)  # (atomic: pytest -n workers may build it together)
     return BENCH
 
 
