@@ -1035,7 +1035,10 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
     int32_t e0 = X0 + eb;
     int32_t e1 = X1 + eb;
     if (FULL) {
-        e1 += (off == lim && lane == 63) ? 3 : 0;
+        // (a scalar branch, rarely taken: off == lim only where the band meets
+        // the read's end; the lane select cost lane-mask logic on every row:
+        // D -0.4 %, r04zn)
+        if (__builtin_expect(off == lim, 0)) e1 = writelane(e1, __builtin_amdgcn_readlane(e1, 63) + 3, 63);
     } else {
         if ((uint32_t)c.L2 == m - 1) e0 += 3;
         if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
