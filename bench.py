@@ -489,7 +489,20 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+
+        # gloo's C++ side prints "[Gloo] Rank r is connected ..." to stdout
+        # while the group forms: sent to stderr, so rank 0's stdout stays the
+        # one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     os.makedirs(args.out_dir, exist_ok=True)
 
     import ccsx_amd as cx
