@@ -23,7 +23,12 @@ Beside it, on the same device:
     as K launches with inputs resident, its own roofline;
   * `e2e`: 16,384 config-E ZMWs through ccsx_gpu_run from host buffers;
   * `cpu_baseline` (rank 0, N = 1): oracle/ccsx_cpu -A -j N on a 1,000-ZMW
-    sample of the same config-E workload, plus config A (BASELINE configs[0]).
+    sample of the same config-E workload, plus config A (BASELINE configs[0]);
+  * `one_process` (rank 0, N > 1): the same 500,000 ZMWs through ONE ccsx
+    process driving all N GPUs (CCSX_NGPU=N: host-side dispatch and ordered
+    gather), the ranks' inputs concatenated, its sample checked likewise.
+Each rank's CLI and generator get the node's CPU share / LOCAL_WORLD_SIZE
+threads, bound to a disjoint CPU slice when N > 1 (rank_cpus).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D|E|H|HP] [--e-zmws 0]
 
@@ -78,6 +83,7 @@ E_LAUNCH_HOLE0 = 10_000_000  # the roofline / e2e lines' config-E holes
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 OPS_PER_CELL = 10
 CLI = os.path.join(ROOT, "ccsx_amd", "bin", "ccsx")
+ORIG_AFFINITY = os.sched_getaffinity(0)  # restored after a rank's CLI ran bound to its slice
 SYNTH_FA = os.path.join(ROOT, "tools", "synth_fa")
 
 
@@ -170,6 +176,56 @@ def cpu_share():
     return max(1, min(affinity, share) if share else affinity), affinity, quota
 
 
+def numa_cpulists():
+    """CPU lists of the NUMA nodes (sysfs), [] where unreadable."""
+    nodes = []
+    base = "/sys/devices/system/node"
+    try:
+        names = sorted((d for d in os.listdir(base) if d.startswith("node") and d[4:].isdigit()), key=lambda d: int(d[4:]))
+    except OSError:
+        return []
+    for d in names:
+        try:
+            with open(os.path.join(base, d, "cpulist")) as f:
+                spec = f.read().strip()
+        except OSError:
+            continue
+        cpus = []
+        for part in filter(None, spec.split(",")):
+            lo, _, hi = part.partition("-")
+            cpus.extend(range(int(lo), int(hi or lo) + 1))
+        nodes.append(cpus)
+    return nodes
+
+
+def rank_cpus(local: int, local_world: int, share: int | None = None, affinity=None, nodes=None):
+    """(threads, CPU list) of one local rank's CLI and generator: the job's CPU
+    share split over the ranks of the node (each rank's CLI otherwise sizes
+    itself to the whole share: local_world-fold oversubscription), and, with
+    more than one local rank, a disjoint slice of the allowed CPUs to bind to
+    -- ranks dealt over the NUMA nodes in order (GPUs are enumerated in NUMA
+    order on the usual nodes), consecutive ranks of a node on consecutive
+    slices.  One rank: no binding (None), as in the single-GPU runs."""
+    if share is None:
+        share = cpu_share()[0]
+    per = max(1, share // max(1, local_world))
+    if local_world <= 1:
+        return per, None
+    allowed = sorted(affinity if affinity is not None else os.sched_getaffinity(0))
+    aset = set(allowed)
+    nodes = [c for c in ([[x for x in n if x in aset] for n in (nodes if nodes is not None else numa_cpulists())]) if c]
+    if not nodes:
+        nodes = [allowed]
+    node = local * len(nodes) // local_world
+    peers = [r for r in range(local_world) if r * len(nodes) // local_world == node]
+    k, pool = peers.index(local), nodes[node]
+    if len(pool) >= per * len(peers):
+        cpus = pool[k * per:(k + 1) * per]
+    else:
+        cpus = pool[k * len(pool) // len(peers):(k + 1) * len(pool) // len(peers)] or pool
+    return per, cpus
+
+
 def read_records(path, want: set, scan: dict):
     """Read a CCS FASTA (a FIFO while the CLI writes it): record count, input
     (hole) order, and the sequences of the holes in `want`."""
@@ -251,14 +307,44 @@ def cli_cells(log_path: str) -> int:
     return 0
 
 
-def cli_line(args, rank: int, world: int, local: int, ndev: int, sharing: int, dist, out_dir: str):
-    """The headline: config E through the CLI, this rank's hole range."""
+E_BYTES_PER_ZMW = 132e3 * 1.15  # config-E FASTA bytes per ZMW, with a margin (65.7 GB per 500k)
+
+
+def input_disk_need(n: int, local_world: int) -> int:
+    """Free bytes a rank needs to write its n-ZMW input: every local rank
+    writes its input to the same disk at once, plus a 4 GiB margin."""
+    return int(n * E_BYTES_PER_ZMW) * max(1, local_world) + (4 << 30)
+
+
+def cpu_ranges(cpus) -> str:
+    """'0-7,16-23' for a CPU list."""
+    out, cpus = [], sorted(cpus)
+    i = 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(f"{cpus[i]}-{cpus[j]}" if j > i else str(cpus[i]))
+        i = j + 1
+    return ",".join(out)
+
+
+def cli_line(args, rank: int, world: int, local: int, local_world: int, ndev: int, sharing: int, dist, out_dir: str):
+    """The headline: config E through the CLI, this rank's hole range.  The
+    rank's CLI and generator get its share of the node's CPUs (rank_cpus),
+    bound to its own CPU slice when several ranks share the node.  Returns
+    (result, input path or None, temp dir): the input is kept for the
+    one-process line (the caller removes the temp dir)."""
     holes = e_rank_range(args.e_zmws, rank, world)
     n = len(holes)
-    threads, _, _ = cpu_share()
+    threads, cpus = rank_cpus(local, local_world)
+    if cpus:
+        # children inherit the binding (no preexec_fn: the FIFO reader is a thread)
+        os.sched_setaffinity(0, cpus)
     env = cli_child_env(local, ndev, sharing)
     tmp = tempfile.mkdtemp(prefix="ccsx_bench_e_", dir=os.environ.get("TMPDIR"))
-    res = {"zmws": n, "hole0": holes.start, "jobs": threads}
+    res = {"zmws": n, "hole0": holes.start, "jobs": threads, "cpus": cpu_ranges(cpus) if cpus else "unbound"}
+    fa = None
     try:
         # W untimed warmup steps: the same CLI on W x 1,024 other config-E
         # ZMWs (its device memory share quartered, so the driver's clearing
@@ -276,8 +362,7 @@ def cli_line(args, rank: int, world: int, local: int, ndev: int, sharing: int, d
         # the input, generated before the timed region (a file; a generator
         # pipe if the disk cannot hold it, whose rate then bounds the run)
         fa = os.path.join(tmp, "e.fa")
-        need = int(n * 132e3 * 1.15)
-        pipe = shutil.disk_usage(tmp).free < need + (4 << 30)
+        pipe = shutil.disk_usage(tmp).free < input_disk_need(n, local_world)
         gen = [SYNTH_FA, str(n), str(holes.start), "0", "0", str(threads)]
         t0 = time.perf_counter()
         if not pipe:
@@ -301,8 +386,68 @@ def cli_line(args, rank: int, world: int, local: int, ndev: int, sharing: int, d
         res["cells"] = cli_cells(log)
         res["sample_holes"] = sample
         res["sample_got"] = scan["got"]
-    finally:
+    except BaseException:
         shutil.rmtree(tmp, ignore_errors=True)
+        raise
+    finally:
+        if cpus:
+            os.sched_setaffinity(0, ORIG_AFFINITY)
+    return res, (None if pipe else fa), tmp
+
+
+def concat_parts(parts, dst: str) -> None:
+    """The per-rank inputs, in rank (= hole) order, into one file; each part
+    is removed once appended, so the disk holds the whole input plus one part."""
+    with open(dst, "wb") as out:
+        for p in parts:
+            with open(p, "rb") as src:
+                size = os.fstat(src.fileno()).st_size
+                off = 0
+                try:
+                    while off < size:
+                        k = os.copy_file_range(src.fileno(), out.fileno(), size - off)
+                        if k <= 0:
+                            break
+                        off += k
+                except OSError:
+                    pass
+                if off < size:  # no in-kernel copy here: the rest by read / write
+                    src.seek(off)
+                    shutil.copyfileobj(src, out, 16 << 20)
+            os.remove(p)
+
+
+def one_process_line(args, world: int, parts, sample, out_dir: str, tmp: str):
+    """N > 1, rank 0: the whole config-E input (the ranks' inputs concatenated
+    in hole order) through ONE ccsx process driving all N GPUs (CCSX_NGPU=N:
+    the CLI's host-side dispatch of micro-batches to per-GPU contexts and its
+    ordered gather, main.c:698-717 / kthread.c:24-46), on the job's whole CPU
+    share, timed from process start to exit like the per-rank line, with its
+    output checked for count and input order and the same sampled holes kept
+    for the oracle comparison."""
+    share, _, _ = cpu_share()
+    res = {"zmws": args.e_zmws, "jobs": share, "ngpu": world}
+    if any(p is None for p in parts):
+        res["skipped"] = "a rank streamed its input from a generator pipe (no disk room for the inputs)"
+        return res
+    largest = max(os.path.getsize(p) for p in parts)
+    if shutil.disk_usage(tmp).free < largest + (4 << 30):
+        res["skipped"] = "no disk room to concatenate the inputs"
+        return res
+    full = os.path.join(tmp, "e_all.fa")
+    t0 = time.perf_counter()
+    concat_parts(parts, full)
+    res["concat_s"] = round(time.perf_counter() - t0, 3)
+    res["input_bytes"] = os.path.getsize(full)
+    env = dict(os.environ, CCSX_NGPU=str(world), CCSX_TIMING="1")
+    log = os.path.join(out_dir, "cli_one_process.log")
+    try:
+        dt, scan = run_cli(full, args.e_zmws, set(sample), env, share, log)
+    finally:
+        os.remove(full)
+    res.update({"cli_s": round(dt, 3), "value": round(args.e_zmws / dt, 3), "unit": "ZMWs/s",
+                "records": scan["nrec"], "records_in_input_order": scan["in_order"], "cells": cli_cells(log),
+                "sample_got": scan["got"]})
     return res
 
 
@@ -314,7 +459,8 @@ def oracle_check(pairs, threads: int):
     return sum(1 for (_, g), w in zip(pairs, want) if g == w)
 
 
-def cpu_baseline(sample_holes, sample_got, threads: int | None = None, sample_j1: int = 60, timed: bool = True):
+def cpu_baseline(sample_holes, sample_got, threads: int | None = None, sample_j1: int = 60, timed: bool = True,
+                 others=None):
     """The CPU leg: oracle/ccsx_cpu (the product's ingest + ccs_prepare around
     the oracle's scalar POA, ccsx's chunked pipeline, -j threads with kt_for's
     dynamic sharing) -- a stand-in for `ccsx -A -j N`, unbuildable here
@@ -324,7 +470,9 @@ def cpu_baseline(sample_holes, sample_got, threads: int | None = None, sample_j1
     CLI's for those holes (the checker).  Then config A (BASELINE configs[0],
     1,000 ZMWs x 10 kb x 8 passes) and -j 1 on a `sample_j1`-ZMW prefix of it
     for the per-core rate.  -j N = the CPUs the process may use (the
-    reference's -j goes straight to kt_for, main.c:794-795)."""
+    reference's -j goes straight to kt_for, main.c:794-795).  `others`: more
+    {name: {hole: CCS}} outputs of the same holes (the one-process line),
+    each compared with the same oracle run."""
     from tools.gen_synth import write
     exe = os.path.join(ROOT, "oracle", "ccsx_cpu")
     if not os.path.exists(exe):
@@ -352,7 +500,11 @@ def cpu_baseline(sample_holes, sample_got, threads: int | None = None, sample_j1
         subprocess.run([exe, "-A", "-j", str(threads), se, se + ".ccs.fa"], check=True)
         dt = time.perf_counter() - t
         cpu_ccs = ccs_of(se + ".ccs.fa")
-        equal = sum(1 for h in sample_holes if cpu_ccs.get(h, b"") == sample_got.get(h, b"") and h in cpu_ccs)
+        def n_equal(got):
+            return sum(1 for h in sample_holes if cpu_ccs.get(h, b"") == got.get(h, b"") and h in cpu_ccs)
+
+        equal = n_equal(sample_got)
+        others_equal = {k: n_equal(g) for k, g in (others or {}).items()}
         res = {"value": round(len(sample_holes) / dt, 3), "unit": "ZMWs/s", "cores": threads, "kind": "port",
                "affinity": affinity, "cgroup_cpu_quota": quota, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
                "nproc": os.cpu_count(), "wall_s": round(dt, 3),
@@ -363,6 +515,8 @@ def cpu_baseline(sample_holes, sample_got, threads: int | None = None, sample_j1
                          f"OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS')}; nproc={os.cpu_count()}) in {dt:.2f} s; "
                          f"{equal}/{len(sample_holes)} CCS byte-equal to the GPU CLI's. A scalar C restatement of "
                          "SPEC.md + main.c, not bsalign's SIMD code (ccsx itself is unbuildable here)"}
+        if others_equal:
+            res["sample_equal_others"] = others_equal
         if timed:
             fa, fa1 = os.path.join(d, "a.fa"), os.path.join(d, "a1.fa")
             write(fa, 1000, 10000, 8, seed=SEED)
@@ -478,6 +632,8 @@ def main():
                                                          "2 throughput; -1: by slice size)")
     ap.add_argument("--wg-cap", type=int, default=0, help="measurement: at most this many workgroups per CU (0: off)")
     ap.add_argument("--out-dir", default=os.path.join(ROOT, "gpurun_out", "bench"), help="CLI logs")
+    ap.add_argument("--no-one-process", dest="one_process", action="store_false",
+                    help="N > 1: skip rank 0's one-process line (one CLI over all N GPUs)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.nzmw:
@@ -526,7 +682,7 @@ def main():
     overrides = {k: os.environ[k] for k in ("CCSX_LIB",) if os.environ.get(k)}
     if args.wg_cap:
         overrides["wg_cap"] = args.wg_cap
-    threads, _, _ = cpu_share()
+    threads = rank_cpus(local, local_world)[0]  # this rank's part of the node's CPU share
 
     # config B (or --config): K launches, inputs resident
     kline = None
@@ -573,9 +729,21 @@ def main():
     del ebatch
 
     cli = None
+    one = None
     if args.e_zmws:
-        cli = cli_line(args, rank, world, local, ndev, sharing, dist, args.out_dir)
-        cli_s, cells_all = aggregate(dist, cli["cli_s"], cli["cells"])
+        cli, part, tmp = cli_line(args, rank, world, local, local_world, ndev, sharing, dist, args.out_dir)
+        try:
+            cli_s, cells_all = aggregate(dist, cli["cli_s"], cli["cells"])
+            if dist is not None and args.one_process:
+                # the ranks' inputs to rank 0, which runs them through one CLI
+                # on all N GPUs while the other ranks wait
+                parts = [None] * world
+                dist.all_gather_object(parts, part)
+                if rank == 0:
+                    one = one_process_line(args, world, parts, cli["sample_holes"], args.out_dir, tmp)
+                dist.barrier()
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
 
     if rank == 0:
         out = {"metric": "CCS ZMWs/sec (whole node)"}
@@ -591,7 +759,14 @@ def main():
                                                               "no collectives",
                            "step": f"1/{args.steps} of each rank's config-E ZMWs; the CLI streams the {args.steps} "
                                    "slices back to back in one process, timed from its start to its exit",
-                           "cli_jobs": cli["jobs"]},
+                           "cli_jobs": cli["jobs"], "cli_cpus": cli["cpus"]},
+                # steps / ms_per_step are nominal: ONE CLI process per rank is
+                # timed from its start to its exit, and ms_per_step x steps is
+                # that whole time (no per-step clock); warmup = one separate,
+                # smaller CLI run (warmup x 1,024 ZMWs) before the input is made
+                "steps_nominal": True,
+                "timed_region": "one ccsx process per rank, start to exit (max over ranks); "
+                                "ms_per_step = that time / steps",
                 "gcups": round(cells_all / cli_s / 1e9, 3),
                 "cli": {k: v for k, v in cli.items() if k not in ("sample_holes", "sample_got")},
             })
@@ -635,23 +810,33 @@ def main():
             out["e2e"] = e2e
         # the checker / CPU leg (outside every timed region)
         if not args.no_cpu_baseline or cli is not None or e2e is not None:
-            from ccsx_amd import prepare, synth_zmw
+            from ccsx_amd import synth_zmw
+            from oracle.oracle import prepare as oracle_prepare  # the checker's own ccs_prepare
             if e2e is not None:
-                pairs = [(prepare(synth_zmw(SEED, h, *zmw_shape(CONFIGS["E"], h))[0]), e2e_kept[i])
+                pairs = [(oracle_prepare(synth_zmw(SEED, h, *zmw_shape(CONFIGS["E"], h))[0]), e2e_kept[i])
                          for h, i in zip(e2e_holes, e2e_keep)]
                 e2e["sample"] = len(pairs)
                 e2e["sample_equal"] = oracle_check(pairs, threads)
             if cli is not None:
+                others = {"one_process": one["sample_got"]} if one is not None and "sample_got" in one else None
                 cb = cpu_baseline(cli["sample_holes"], cli["sample_got"],
-                                  timed=world == 1 and not args.no_cpu_baseline)
+                                  timed=world == 1 and not args.no_cpu_baseline, others=others)
                 out["cli"]["sample"] = cb["sample_zmws"]
                 out["cli"]["sample_equal"] = cb["sample_equal_to_gpu_cli"]
+                if one is not None:
+                    out["one_process"] = {k: v for k, v in one.items() if k != "sample_got"}
+                    if others:
+                        out["one_process"]["sample"] = cb["sample_zmws"]
+                        out["one_process"]["sample_equal"] = cb["sample_equal_others"]["one_process"]
                 if world == 1 and not args.no_cpu_baseline:
                     out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
         bad = []
         if cli is not None and out["cli"]["sample_equal"] != out["cli"]["sample"]:
             bad.append("CLI sample")
+        op = out.get("one_process", {})
+        if "sample" in op and op["sample_equal"] != op["sample"]:
+            bad.append("one-process CLI sample")
         if e2e is not None and e2e.get("sample_equal") != e2e.get("sample"):
             bad.append("e2e sample")
         if bad:

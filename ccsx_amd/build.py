@@ -162,7 +162,9 @@ def build_product(verbose: bool = False) -> str:
 
 
 def build_oracle(verbose: bool = False) -> str:
-    srcs = [os.path.join(ORACLE_DIR, f) for f in sorted(os.listdir(ORACLE_DIR)) if f.endswith(".c") and f.startswith("poa_")]
+    # the POA restatement (poa_*.c) and the ccs_prepare one (prep_oracle.c)
+    srcs = [os.path.join(ORACLE_DIR, f) for f in sorted(os.listdir(ORACLE_DIR))
+            if f.endswith(".c") and (f.startswith("poa_") or f.startswith("prep_"))]
     hdrs = [os.path.join(ORACLE_DIR, f) for f in os.listdir(ORACLE_DIR) if f.endswith(".h")]
     if _stale(ORACLE_LIB, srcs + hdrs):
         cmd = ["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-o", ORACLE_LIB] + srcs + ["-lpthread", "-lz"]

@@ -775,7 +775,12 @@ static int plan_slots(ccsx_ctx *c, uint64_t &slot_budget)
     slot_budget = c->slot_budget ? c->slot_budget : std::max<uint64_t>(1ull << 29, budget / 2);
     if (c->prealloc) {
         const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
-        for (Slot &s : c->slot)
+        // only idle slots: a slot whose batch is still running keeps its
+        // workspace (growing it would free the memory under that kernel; the
+        // slot is grown by the next plan that finds it idle)
+        for (int k = 0; k < 2; ++k) {
+            Slot &s = c->slot[k];
+            if (c->tk[k].pending || s.inflight) continue;
             if (s.d_ws.cap < slot_budget) {
                 const auto t0 = std::chrono::steady_clock::now();
                 HIPCHK(c, s.d_ws.reserve(slot_budget, true));
@@ -784,6 +789,7 @@ static int plan_slots(ccsx_ctx *c, uint64_t &slot_budget)
                             slot_budget / 1e9,
                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
             }
+        }
     }
     return 0;
 }

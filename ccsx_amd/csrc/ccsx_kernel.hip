@@ -168,6 +168,28 @@ __device__ __forceinline__ uint32_t enc_base(uint32_t c)
 // ----------------------------------------------------------------------------
 // per-ZMW state
 // ----------------------------------------------------------------------------
+// Per-ZMW phase counters (KArgs::prof): only the profiling builds carry them
+// (-DCCSX_PROF or -DCCSX_TB_COUNT, and the diagnostic library's -DCCSX_DP_STAMPS).  In the
+// product they were ~10 live 64-bit counters for the whole kernel -- SGPRs
+// the DP and merge spilled for (tools/spill_attr.py); there every counter is
+// a sink and KArgs::prof receives zeros.
+#if defined(CCSX_PROF) || defined(CCSX_DP_STAMPS) || defined(CCSX_TB_COUNT)
+constexpr bool kProfiling = true;
+typedef unsigned long long Prof[kProfSlots];
+#else
+constexpr bool kProfiling = false;
+struct PfSink {
+    template <class T>
+    __device__ PfSink &operator+=(T) { return *this; }
+    template <class T>
+    __device__ PfSink &operator=(T) { return *this; }
+    __device__ operator unsigned long long() const { return 0ull; }
+};
+struct Prof {
+    __device__ PfSink operator[](int) const { return PfSink{}; }
+};
+#endif
+
 struct Z {
     ZmwDesc d;
     ZLayout L;
@@ -187,10 +209,13 @@ struct Z {
     uint32_t R, E;
     int32_t status;
     unsigned long long cells;
-    unsigned long long pf[kProfSlots];
+    Prof pf;
 };
 
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
+// the phase clock of the profiling builds; 0 in the product (no s_memtime)
+__device__ __forceinline__ unsigned long long pstamp() { return kProfiling ? stamp() : 0ull; }
+__device__ __forceinline__ unsigned long long prealtime() { return kProfiling ? __builtin_amdgcn_s_memrealtime() : 0ull; }
 
 // Raw buffer access: lanes whose byte offset is >= `bytes` are discarded
 // (stores) or read 0 (loads) by the hardware, so a masked store is still one
@@ -2522,20 +2547,20 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             z.status = kErrReadLen;
             return 0;
         }
-        unsigned long long t0 = stamp();
+        unsigned long long t0 = pstamp();
         if (!staged || zseq != z.seq) load_read(z, zseq + uni(rdoff[k]), m);
-        unsigned long long t1 = stamp();
+        unsigned long long t1 = pstamp();
         z.pf[kPfLoad] += t1 - t0;
         if (z.R) {
             uint32_t er, ej;
             z.pf[kPfRows] += z.R;
             dp_align(z, m, er, ej);
             if (z.status) return 0;
-            unsigned long long t2 = stamp();
+            unsigned long long t2 = pstamp();
             z.pf[kPfDp] += t2 - t1;
             traceback(z, m, er, ej);
             if (z.status) return 0;
-            t1 = stamp();
+            t1 = pstamp();
             z.pf[kPfTrace] += t1 - t2;
         }
         {
@@ -2549,11 +2574,11 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
         }
         if (z.status) return 0;
         staged = k + 1 < z.d.n;  // (the merge staged read k + 1 under run_poa's own checks)
-        z.pf[kPfMerge] += stamp() - t1;
+        z.pf[kPfMerge] += pstamp() - t1;
     }
-    unsigned long long t3 = stamp();
+    unsigned long long t3 = pstamp();
     const uint32_t nc = call_columns(z, n);
-    z.pf[kPfColumns] += stamp() - t3;
+    z.pf[kPfColumns] += pstamp() - t3;
     return nc;
 }
 
@@ -2693,7 +2718,7 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
     z.cells = 0;
 #pragma unroll
     for (int i = 0; i < kProfSlots; ++i) z.pf[i] = 0;
-    if (threadIdx.x >= 64) {
+    if (kHelpers > 0 && threadIdx.x >= 64) {
         // waves 1 and 2: the decision bits of the even / odd rows of every DP
         const uint32_t h = uni(threadIdx.x >> 6) - 1u;
         dp_helper(z, h);
@@ -2708,9 +2733,9 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
     // of other workgroups, whose DP work has a block of slack: let wave 0 win
     // the issue arbitration (measured: 63.9 -> 58.4 ms per launch, config B)
     __builtin_amdgcn_s_setprio(kPrioWave0);
-    const unsigned long long t_start = stamp();
-    z.pf[kPfStartRt] = __builtin_amdgcn_s_memrealtime();
-    z.pf[kPfHw0] = wave_hw_id();
+    const unsigned long long t_start = pstamp();
+    z.pf[kPfStartRt] = prealtime();
+    if (kProfiling) z.pf[kPfHw0] = wave_hw_id();
     const uint32_t n = z.d.n;
     const uint32_t *soff = a.soff + z.d.seg0, *slen = a.slen + z.d.seg0;
     uint32_t *rdoff = P<uint32_t>(z, z.L.rdoff), *rdlen = P<uint32_t>(z, z.L.rdlen);
@@ -2758,9 +2783,9 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
                     i = ncols;
                     break;
                 }
-                const unsigned long long tb0 = stamp();
+                const unsigned long long tb0 = pstamp();
                 i = find_breakpoint(z, ncols, n, colrate);
-                z.pf[kPfShred] += stamp() - tb0;
+                z.pf[kPfShred] += pstamp() - tb0;
                 if (i >= 1) break;
             }
             if (z.status) break;
@@ -2772,9 +2797,9 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
                 }
                 ++nround;
             }
-            const unsigned long long te0 = stamp();
+            const unsigned long long te0 = pstamp();
             emit(z, i, ncols, n, flag, out, ol);
-            z.pf[kPfShred] += stamp() - te0;
+            z.pf[kPfShred] += pstamp() - te0;
         }
         if (a.bplog) {
             if (nround > z.d.bpcap && !z.status) z.status = kErrBpLog;
@@ -2787,8 +2812,8 @@ __device__ __forceinline__ void zmw_body(const KArgs &a, int32_t *smem)
         a.status[zi] = z.status;
         a.cells[zi] = z.cells;
         if (a.prof) {
-            z.pf[kPfTotal] = stamp() - t_start;
-            z.pf[kPfEndRt] = __builtin_amdgcn_s_memrealtime();
+            z.pf[kPfTotal] = pstamp() - t_start;
+            z.pf[kPfEndRt] = prealtime();
 #pragma unroll
             for (int i = 0; i < kProfSlots; ++i) a.prof[(size_t)zi * kProfSlots + i] = z.pf[i];
         }

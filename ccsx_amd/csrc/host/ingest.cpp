@@ -142,6 +142,18 @@ struct MmapSource : ByteSource {
     {
         stop = true;
         if (toucher.joinable()) toucher.join();
+        // the block may outlive the source (a parser still holds it): leave
+        // it only the part still mapped, so its destructor never unmaps the
+        // released prefix, where unrelated mappings may live by now
+        std::lock_guard<std::mutex> g(rel_m);
+        if (b->map && released) {
+            if (released >= b->map_len) {
+                b->map = nullptr, b->map_len = 0;
+            } else {
+                b->map = static_cast<char *>(b->map) + released;
+                b->map_len -= released;
+            }
+        }
     }
     std::shared_ptr<Block> next() override { return b; }
 };

@@ -42,6 +42,10 @@
 
 namespace {
 
+// ZMWs the reader takes into the first chunk before it waits for the device
+// contexts to fix the chunk sizes
+constexpr size_t kChunkProvisional = 16384;
+
 // Bases of a chunk's ZMWs live in one arena per chunk (an anonymous mapping
 // with transparent huge pages), recycled through a pool: per-ZMW strings
 // (~130 KB each, ~2 GB per 16,384-ZMW chunk) cost a page fault per 4 KB page
@@ -550,6 +554,10 @@ int main(int argc, char **argv)
 
     // test hook: the device reports this hole as failed (tests/test_gpu_cli.py)
     const std::string fault_hole = getenv("CCSX_FAULT_HOLE") ? getenv("CCSX_FAULT_HOLE") : "";
+    // test hook: batches after the first CCSX_FATAL_AFTER ones fail as a
+    // context error does (the fatal path's teardown, tests/test_gpu_cli.py)
+    const long fatal_after = getenv("CCSX_FATAL_AFTER") ? atol(getenv("CCSX_FATAL_AFTER")) : -1;
+    std::atomic<long> batches_seen(0);
 
     // step 1, device side: one worker per context
     // a batch in flight on a context: its input arrays live until collected
@@ -574,6 +582,7 @@ int main(int argc, char **argv)
     // results of a batch (r: the run / collect status) into its chunk
     auto finish = [&](int w, Flight &f, int r) {
         Chunk &ch = *f.b.chunk;
+        if (fatal_after >= 0 && batches_seen.fetch_add(1) >= fatal_after) r = -9;
         if (r == 0 || r == -2) {
             // -2: some ZMWs failed on the device, the rest are valid
             uint64_t cells = 0;
@@ -590,7 +599,7 @@ int main(int argc, char **argv)
             }
         } else if (!fatal.exchange(true)) {
             std::lock_guard<std::mutex> g(err_m);
-            fprintf(stderr, "[ccsx] device context %d: %s\n", w, ccsx_gpu_error(ctx[w]));
+            fprintf(stderr, "[ccsx] device context %d: %s\n", w, r == -9 ? "injected fatal error (test hook)" : ccsx_gpu_error(ctx[w]));
         }
         if (timing)
             fprintf(stderr, "[ccsx] chunk %zu batch of %zu ZMWs on context %d: %.0f-%.0f ms\n", ch.id, f.b.idx.size(),
@@ -705,7 +714,15 @@ int main(int argc, char **argv)
                 if (have_holes && hole_set.count(zr.hole)) continue;
                 zs.emplace_back();
                 zs.back().ref = std::move(zr);
-                const size_t lim = chunk_size ? chunk_size : chunk_first.load();
+                size_t lim = chunk_size ? chunk_size : chunk_first.load();
+                if (lim == SIZE_MAX && zs.size() >= kChunkProvisional) {
+                    // the devices are still opening: wait for the chunk sizes
+                    // rather than grow the first chunk without bound (a slow
+                    // HIP init or 16 contexts would put a page-cached input
+                    // into one chunk and one arena, with no pipelining)
+                    while ((lim = chunk_first.load()) == SIZE_MAX && !fatal)
+                        std::this_thread::sleep_for(std::chrono::microseconds(200));
+                }
                 if (zs.size() >= lim) {
                     chunk_size = std::min(zs.size() * 4, chunk_last.load());
                     break;

@@ -1,7 +1,9 @@
 /*
- * oracle/ccsx_cpu.c -- a CPU-only ccsx: the host program's ingest and
- * ccs_prepare (the product library's C-ABI, include/ccsx_seqio.h and
- * include/ccsx_host.h) around the oracle's POA (oracle/poa_oracle.c).
+ * oracle/ccsx_cpu.c -- a CPU-only ccsx: the host program's ingest (the
+ * product library's C-ABI, include/ccsx_seqio.h, pinned by the reference's own
+ * seqio.h on tests/golden/host) around the oracle's ccs_prepare
+ * (oracle/prep_oracle.c, an independent restatement of main.c:116-453) and
+ * POA (oracle/poa_oracle.c).
  *
  * TEST INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg times it as the
  * stand-in for `ccsx -A -j N` (main.c:723-870), which is unbuildable here
@@ -20,9 +22,9 @@
 #include <time.h>
 #include <unistd.h>
 
-#include "../include/ccsx_host.h"
 #include "../include/ccsx_seqio.h"
 #include "poa_oracle.h"
+#include "prep_oracle.h"
 
 typedef struct {
     char *name;  /* movie/hole */
@@ -56,7 +58,7 @@ static void *worker(void *arg)
             off = realloc(off, cap * 4);
             len = realloc(len, cap * 4);
         }
-        const uint32_t ns = ccsx_prepare_apply(z->seqs, z->lens, z->n, off, len);
+        const uint32_t ns = oprep_prepare_apply(z->seqs, z->lens, z->n, off, len);
         size_t tot = 0;
         for (uint32_t k = 0; k < z->n; ++k) tot += z->lens[k];
         z->ccs = malloc(tot + 16);

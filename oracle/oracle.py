@@ -53,8 +53,64 @@ def lib() -> C.CDLL:
         L.ocsx_zmw_log.restype = C.c_size_t
         L.ocsx_edit_distance.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32]
         L.ocsx_edit_distance.restype = C.c_int64
+        L.oprep_prepare.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
+                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]
+        L.oprep_prepare.restype = C.c_uint32
+        L.oprep_prepare_apply.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_uint32)]
+        L.oprep_prepare_apply.restype = C.c_uint32
+        L.oprep_pairwise.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32]
+        L.oprep_pairwise.restype = OprepAln
         _lib = L
     return _lib
+
+
+class OprepAln(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("qb", "qe", "tb", "te", "score", "mat", "mis", "ins", "del_", "aln")]
+
+
+class Prepared:
+    """One ZMW after the oracle's ccs_prepare + strand flip (the same fields as
+    ccsx_amd.Prepared: segments are slices of seqs)."""
+
+    def __init__(self, seqs: bytes, offs, lens):
+        self.seqs, self.offs, self.lens = seqs, offs, lens
+
+
+def _p32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def prepare_segments(subreads: list[bytes]):
+    """The oracle's ccs_prepare (main.c:344-453): (offs, lens, reverse flags)
+    of the push list into the concatenated subreads, template first."""
+    seqs = b"".join(subreads)
+    lens = np.ascontiguousarray([len(s) for s in subreads], dtype=np.uint32)
+    n = len(subreads)
+    so = np.zeros(max(n, 1), np.uint32)
+    sl = np.zeros(max(n, 1), np.uint32)
+    rv = np.zeros(max(n, 1), np.uint8)
+    ns = lib().oprep_prepare(seqs, _p32(lens), n, _p32(so), _p32(sl), rv.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return so[:ns].copy(), sl[:ns].copy(), rv[:ns].copy()
+
+
+def prepare(subreads: list[bytes]) -> Prepared:
+    """The oracle's ccs_prepare + in-place reverse complement of the reverse
+    segments (seqio.h:138-148): what the POA is pushed."""
+    seqs = b"".join(subreads)
+    buf = C.create_string_buffer(seqs, len(seqs) + 1)
+    lens = np.ascontiguousarray([len(s) for s in subreads], dtype=np.uint32)
+    n = len(subreads)
+    so = np.zeros(max(n, 1), np.uint32)
+    sl = np.zeros(max(n, 1), np.uint32)
+    ns = lib().oprep_prepare_apply(buf, _p32(lens), n, _p32(so), _p32(sl))
+    return Prepared(buf.raw[:len(seqs)], so[:ns].copy(), sl[:ns].copy())
+
+
+def pairwise(q: bytes, t: bytes) -> dict:
+    """SPEC.md §8's aligner as the oracle restates it (2-bit codes in q, t)."""
+    r = lib().oprep_pairwise(q, len(q), t, len(t))
+    return {n if n != "del_" else "del": getattr(r, n) for n, _ in OprepAln._fields_}
 
 
 def edit_identity(a: bytes, b: bytes, band: int = 1024) -> float:

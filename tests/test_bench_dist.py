@@ -102,6 +102,16 @@ def test_bench_two_ranks_on_device():
     assert two["value"] > 0 and two["e2e"]["value"] > 0
     assert two["e2e"]["sample_equal"] == two["e2e"]["sample"] == 64
     assert one["roofline"]["kernel_cfg"] in (0, 1, 3) and one["scaling"] == "strong"
+    # the job's CPU share split over the two local ranks, each bound
+    share = bench.cpu_share()[0]
+    assert one["config"]["cli_jobs"] == share and one["config"]["cli_cpus"] == "unbound"
+    assert two["config"]["cli_jobs"] == max(1, share // 2) and two["config"]["cli_cpus"] != "unbound"
+    # N > 1: rank 0's one-process line over the whole input, all ranks' GPUs
+    op = two["one_process"]
+    assert "skipped" not in op, op
+    assert op["records"] == 600 and op["records_in_input_order"] and op["ngpu"] == 2
+    assert op["sample_equal"] == op["sample"] == 12
+    assert "one_process" not in one
 
 
 def test_e_rank_ranges_split_the_config():
@@ -110,3 +120,50 @@ def test_e_rank_ranges_split_the_config():
         assert sum(len(r) for r in rs) == 500_000
         assert all(a.stop == b.start for a, b in zip(rs, rs[1:]))
         assert rs[0].start == bench.E_HOLE0 and max(map(len, rs)) - min(map(len, rs)) <= 1
+
+
+def test_rank_cpus_split_the_share_over_local_ranks():
+    """LOCAL_WORLD_SIZE = 8 on a node whose job share is 128 CPUs of 256
+    (two NUMA nodes): each rank's CLI and generator get 128 / 8 = 16 threads,
+    bound to disjoint slices, four ranks per NUMA node in rank order."""
+    nodes = [list(range(0, 64)) + list(range(128, 192)), list(range(64, 128)) + list(range(192, 256))]
+    seen = set()
+    for local in range(8):
+        t, cpus = bench.rank_cpus(local, 8, share=128, affinity=range(256), nodes=nodes)
+        assert t == 16 and len(cpus) == 16
+        assert set(cpus) <= set(nodes[local * 2 // 8])
+        assert not seen & set(cpus)
+        seen |= set(cpus)
+    # one rank: the whole share, no binding (the single-GPU runs as before)
+    assert bench.rank_cpus(0, 1, share=16, affinity=range(256), nodes=nodes) == (16, None)
+    # the one-GPU box's two-rank rehearsal: 16 CPUs of quota -> 8 per rank
+    t0, c0 = bench.rank_cpus(0, 2, share=16, affinity=range(256), nodes=[])
+    t1, c1 = bench.rank_cpus(1, 2, share=16, affinity=range(256), nodes=[])
+    assert t0 == t1 == 8 and not set(c0) & set(c1)
+    # fewer CPUs than ranks x threads: still disjoint, never empty
+    for local in range(4):
+        t, cpus = bench.rank_cpus(local, 4, share=64, affinity=range(8), nodes=[])
+        assert t == 16 and len(cpus) == 2
+    assert bench.cpu_ranges([0, 1, 2, 5, 7, 8]) == "0-2,5,7-8"
+
+
+def test_disk_need_counts_every_local_input():
+    one = bench.input_disk_need(62_500, 1)
+    eight = bench.input_disk_need(62_500, 8)
+    margin = 4 << 30
+    assert eight - margin == 8 * (one - margin)
+    # the whole config E split over 8 ranks needs the whole 65.7 GB at once
+    assert eight - margin >= 65.7e9
+
+
+def test_concat_parts_in_rank_order(tmp_path):
+    parts = []
+    for r in range(3):
+        p = tmp_path / f"p{r}.fa"
+        p.write_bytes(b">m/%d/0_10\nACGT\n" % r * (1000 + r))
+        parts.append(str(p))
+    want = b"".join(open(p, "rb").read() for p in parts)
+    dst = str(tmp_path / "all.fa")
+    bench.concat_parts(parts, dst)
+    assert open(dst, "rb").read() == want
+    assert not any(os.path.exists(p) for p in parts)

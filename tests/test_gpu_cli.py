@@ -8,6 +8,7 @@ import pytest
 
 import ccsx_amd as cx
 from oracle.oracle import batch
+from oracle.oracle import prepare as oracle_prepare
 from tools.gen_synth import records, write, write_bam
 
 pytestmark = pytest.mark.gpu
@@ -15,12 +16,13 @@ BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 
 
 def _expected(path, mode, min_count=3, mn=5000, mx=500000, exclude=(), is_bam=False):
-    """The oracle on the same records, filters and push lists as the CLI."""
+    """The oracle on the same records and filters as the CLI, with its own
+    ccs_prepare (oracle/prep_oracle.c, independent of the CLI's host/prepare.cpp)."""
     keep = []
     for movie, hole, subs in cx.read_zmws(path, is_bam):
         if len(subs) < min_count + 2 or not (mn <= sum(map(len, subs)) <= mx) or hole in exclude:
             continue
-        keep.append((movie, hole, cx.prepare(subs)))
+        keep.append((movie, hole, oracle_prepare(subs)))
     ccs, _, _ = batch([p for _, _, p in keep], mode, 16)
     return b"".join(b">%s/%s/ccs\n%s\n" % (m.encode(), h.encode(), c) for (m, h, _), c in zip(keep, ccs) if c)
 
@@ -151,8 +153,37 @@ def test_cli_breakpoint_lines(tmp_path):
     got = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("breakpoint=")]
     want = []
     for movie, hole, subs in cx.read_zmws(fa, False):
-        p = cx.prepare(subs)
+        p = oracle_prepare(subs)
         _, bps = Poa().zmw_breakpoints(p.seqs, p.offs, p.lens)
         want += [f"breakpoint={i} maplen={c} nseq={len(p.lens)} hole={hole}" for i, c in bps]
     assert len(want) > 12 and got == want
     assert open(out, "rb").read() == _expected(fa, 0)
+
+
+@pytest.mark.parametrize("fatal", [False, True])
+def test_cli_teardown_after_input_release(tmp_path, fatal):
+    """A mapped input file larger than a few chunks is unmapped behind the
+    reader (ZmwSource::release); the teardown that follows must unmap only
+    what is still mapped (the block's destructor unmapped the whole
+    original range, over whatever the kernel had placed in the released hole).
+    CCSX_EXIT_CLOSE runs the full teardown after a good run; CCSX_FATAL_AFTER
+    fails the third batch as a context error, so the fatal path's teardown
+    (reader, contexts, written chunks) runs after releases too."""
+    fa = str(tmp_path / "in.fa")
+    write(fa, 3000, 1000, 6)
+    out = str(tmp_path / "out.fa")
+    env = dict(CCSX_CHUNK="1024", CCSX_CHUNK0="512", CCSX_SLOTS="1")
+    if fatal:
+        env["CCSX_FATAL_AFTER"] = "2"
+        r = subprocess.run([BIN, "-A", "-j", "4", fa, out], capture_output=True, timeout=300,
+                           env=dict(os.environ, **env))
+        assert r.returncode == 1, r.stderr.decode()[-2000:]
+        assert b"injected fatal error" in r.stderr
+        assert r.returncode >= 0  # no signal (a teardown fault would be -11 / -6)
+    else:
+        env["CCSX_EXIT_CLOSE"] = "1"
+        r = _run(["-A", "-j", "4", fa, out], env=env)
+        assert b"teardown:" in r.stderr
+        got = open(out, "rb").read()
+        assert got.count(b">") == 3000
+        assert got == _expected(fa, 0)
