@@ -28,15 +28,17 @@ extern "C" hipError_t ccsx_launch_zmw_lat(const ccsx::KArgs *a, uint32_t lds_byt
 extern "C" hipError_t ccsx_launch_zmw_occ(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" hipError_t ccsx_launch_zmw_tput(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" hipError_t ccsx_launch_zmw_solo(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+extern "C" hipError_t ccsx_launch_zmw_solo16(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" void ccsx_kcfg_info_lat(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_occ(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_tput(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_solo(ccsx::KCfgInfo *o);
+extern "C" void ccsx_kcfg_info_solo16(ccsx::KCfgInfo *o);
 
 namespace {
 typedef hipError_t (*LaunchFn)(const ccsx::KArgs *, uint32_t, hipStream_t);
 constexpr LaunchFn kLaunch[ccsx::kCfgCount] = {ccsx_launch_zmw_lat, ccsx_launch_zmw_occ, ccsx_launch_zmw_tput,
-                                               ccsx_launch_zmw_solo};
+                                               ccsx_launch_zmw_solo, ccsx_launch_zmw_solo16};
 
 ccsx::KCfgInfo kcfg_info(int cfg)
 {
@@ -44,7 +46,8 @@ ccsx::KCfgInfo kcfg_info(int cfg)
     if (cfg == ccsx::kCfgLatency) ccsx_kcfg_info_lat(&o);
     else if (cfg == ccsx::kCfgOccupancy) ccsx_kcfg_info_occ(&o);
     else if (cfg == ccsx::kCfgThroughput) ccsx_kcfg_info_tput(&o);
-    else ccsx_kcfg_info_solo(&o);
+    else if (cfg == ccsx::kCfgSolo) ccsx_kcfg_info_solo(&o);
+    else ccsx_kcfg_info_solo16(&o);
     return o;
 }
 
@@ -52,12 +55,12 @@ ccsx::KCfgInfo kcfg_info(int cfg)
 // buffer and cursors
 uint32_t kcfg_lds(int cfg, uint32_t extra) { return (kcfg_info(cfg).lds_fixed_words + extra) * 4u; }
 
-// workgroups per CU: 16 waves per CU (128 VGPRs, 4 waves per SIMD) and
-// 160 KiB of LDS
+// workgroups per CU: 4 SIMDs x the object's waves per SIMD (its register
+// budget: 4 at 128 VGPRs, 5 at 96) and 160 KiB of LDS
 uint32_t kcfg_wg_per_cu(int cfg, uint32_t extra)
 {
     const ccsx::KCfgInfo i = kcfg_info(cfg);
-    const uint32_t by_waves = 16u / (i.threads / 64u);
+    const uint32_t by_waves = 4u * i.waves_per_simd / (i.threads / 64u);
     const uint32_t by_lds = (160u * 1024u) / kcfg_lds(cfg, extra);
     return std::min(by_waves, by_lds);
 }
@@ -482,8 +485,16 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
         const size_t res_lat = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgLatency, extra);
         const size_t res_occ = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgOccupancy, extra);
         s.cfg = nz <= res_lat ? ccsx::kCfgLatency : nz < kSoloSliceFactor * res_occ ? ccsx::kCfgOccupancy
-                                                                                  : ccsx::kCfgSolo;
+                                                                                  : ccsx::kCfgSolo16;
         if (c->cfg_force >= 0) s.cfg = c->cfg_force;
+        // solo16 (int16 ring) takes the LDS instance with pushed reads of at
+        // most its max_read bases (a tight-cap shredded slice pushes at most
+        // its read cap); other slices run the solo object, forced or not
+        if (s.cfg == ccsx::kCfgSolo16) {
+            const uint32_t mr = kcfg_info(ccsx::kCfgSolo16).max_read;
+            const uint32_t pushed = shred_tight ? std::min(lmax_all, c->shred_read_cap) : lmax_all;
+            if (!s.lds_read_words || (mr && pushed > mr)) s.cfg = ccsx::kCfgSolo;
+        }
     }
     size_t freeb = 0, totb = 0;
     const auto ti = std::chrono::steady_clock::now();

@@ -346,11 +346,39 @@ __device__ __forceinline__ void load_read(Z &z, const uint8_t *src, uint32_t m)
     wsync();
 }
 
+// The DP ring's cells: int32, or (CCSX_RING16, the solo16 object) int16 --
+// absolute values saturated to int16, exact for reads of at most
+// kRing16MaxRead bases: every real H / D value of such a DP lies in
+// [-2m - 12, 2m] (the read-prefix source term bounds it below, two points per
+// aligned base above), while the -inf class (the kNeg / kNegH sentinels and
+// what they propagate) saturates to -32768, below every real value, so every
+// max the recurrence takes and every tie it breaks between real values is
+// unchanged; a -inf value never wins against the always-real source term of
+// M, so its tags and ext bits are never followed
+#ifdef CCSX_RING16
+typedef int16_t RingT;
+#else
+typedef int32_t RingT;
+#endif
+constexpr uint32_t kRing16MaxRead = 16376;
+// a value as the ring stores it (-inf class: -32768 in the int16 ring)
+__device__ __forceinline__ RingT ring_val(int32_t v) { return sizeof(RingT) == 2 ? (RingT)max(v, -32768) : (RingT)v; }
+// the lane's two adjacent cells (row points at cell 2 lane) of H or D
+__device__ __forceinline__ void ring_store2(RingT *row, int32_t a, int32_t b)
+{
+#ifdef CCSX_RING16
+    *reinterpret_cast<decltype(__builtin_amdgcn_cvt_pk_i16(a, b)) *>(row) = __builtin_amdgcn_cvt_pk_i16(a, b);
+#else
+    *reinterpret_cast<int2 *>(row) = make_int2(a, b);
+#endif
+}
+
 // LDS layout of a workgroup (int32 words)
 // (the solo object has no helpers: no diagnostic slots or band-offset ring,
 // which keeps a config-D workgroup within 10 KB, 16 per CU)
-constexpr int kLdsRing = 0;                              // kRingA DP rows x kRowW (traceback: 2 blocks)
-constexpr int kLdsDiag = kLdsRing + kRingA * kRowW;      // 32: helpers' diagnostic counters at exit
+constexpr int kRingWords = kRingA * kRowW * (int)sizeof(RingT) / 4;  // LDS words of the DP ring area
+constexpr int kLdsRing = 0;                              // kRingA DP rows x kRowW cells (traceback: its blocks)
+constexpr int kLdsDiag = kLdsRing + kRingWords;          // 32: helpers' diagnostic counters at exit
 constexpr int kLdsOffRing = kLdsDiag + (kHelpers ? 32 : 0);  // 64: band offset of DP row q at q & 63
 constexpr int kLdsJob = kLdsOffRing + (kHelpers ? 64 : 0);   // 16: DP job / results
 constexpr int kLdsFixed = kLdsJob + 16;                  // then: the read (nibble pairs), shredding cursors
@@ -515,11 +543,11 @@ __device__ __forceinline__ void pred_fold(PredAcc &A, uint32_t s, uint32_t tag, 
 }
 
 // the five cells of a predecessor row at band shift sh (lane's cells 2l, 2l+1)
-__device__ __forceinline__ void pred_cells(const int32_t *row, int32_t sh, int lane, int32_t &hA, int32_t &hB,
+__device__ __forceinline__ void pred_cells(const RingT *row, int32_t sh, int lane, int32_t &hA, int32_t &hB,
                                            int32_t &hC, int32_t &dB, int32_t &dC)
 {
     if ((uint32_t)(sh + 3) <= 7u) {
-        const int32_t *b = row + kHc - 1 + 2 * lane + sh;
+        const RingT *b = row + kHc - 1 + 2 * lane + sh;
         hA = b[0];
         hB = b[1];
         hC = b[2];
@@ -537,7 +565,7 @@ __device__ __forceinline__ void pred_cells(const int32_t *row, int32_t sh, int l
 
 // the predecessor terms of row r (np <= 4, every predecessor in the ring)
 template <bool SLOTS>
-__device__ __forceinline__ void pred_terms(const int32_t *ring, uint32_t r, int32_t off, uint32_t np, uint32_t p0,
+__device__ __forceinline__ void pred_terms(const RingT *ring, uint32_t r, int32_t off, uint32_t np, uint32_t p0,
                                            uint32_t p1, uint32_t p2, uint32_t p3, int32_t o0, int32_t o1, int32_t o2,
                                            int32_t o3, int lane, PredAcc &A)
 {
@@ -550,10 +578,10 @@ __device__ __forceinline__ void pred_terms(const int32_t *ring, uint32_t r, int3
         // every predecessor within the padded band: issue all reads (absent
         // slots re-read slot 0's row), then fold
         const int L2 = 2 * lane;
-        const int32_t *b0 = ring + (p0 % kRingA) * kRowW + (kHc - 1) + L2 + s0;
-        const int32_t *b1 = np > 1 ? ring + (p1 % kRingA) * kRowW + (kHc - 1) + L2 + s1 : b0;
-        const int32_t *b2 = np > 2 ? ring + (p2 % kRingA) * kRowW + (kHc - 1) + L2 + s2 : b0;
-        const int32_t *b3 = np > 3 ? ring + (p3 % kRingA) * kRowW + (kHc - 1) + L2 + s3 : b0;
+        const RingT *b0 = ring + (p0 % kRingA) * kRowW + (kHc - 1) + L2 + s0;
+        const RingT *b1 = np > 1 ? ring + (p1 % kRingA) * kRowW + (kHc - 1) + L2 + s1 : b0;
+        const RingT *b2 = np > 2 ? ring + (p2 % kRingA) * kRowW + (kHc - 1) + L2 + s2 : b0;
+        const RingT *b3 = np > 3 ? ring + (p3 % kRingA) * kRowW + (kHc - 1) + L2 + s3 : b0;
         constexpr int dd = kDc - kHc + 1;
         const int32_t a0 = b0[0], a1 = b0[1], a2 = b0[2], a3 = b0[dd], a4 = b0[dd + 1];
         const int32_t c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
@@ -586,7 +614,7 @@ __device__ __forceinline__ void pred_terms(const int32_t *ring, uint32_t r, int3
 // within the ring; reads through the padded band when every shift is in
 // [-3, 4], else bounds-checked per cell
 template <int NP, bool SLOTS>
-__device__ __forceinline__ void pred_terms_n(const int32_t *ring, uint32_t r, int32_t off, uint32_t p0, uint32_t p1,
+__device__ __forceinline__ void pred_terms_n(const RingT *ring, uint32_t r, int32_t off, uint32_t p0, uint32_t p1,
                                              int32_t o0, int32_t o1, int lane, PredAcc &A)
 {
     const int32_t s0 = off - o0, s1 = off - o1;
@@ -594,8 +622,8 @@ __device__ __forceinline__ void pred_terms_n(const int32_t *ring, uint32_t r, in
     constexpr int dd = kDc - kHc + 1;
     if (__builtin_expect(inr, 1)) {
         const int L2 = 2 * lane;
-        const int32_t *b0 = ring + (p0 % kRingA) * kRowW + (kHc - 1) + L2 + s0;
-        const int32_t *b1 = ring + (p1 % kRingA) * kRowW + (kHc - 1) + L2 + s1;
+        const RingT *b0 = ring + (p0 % kRingA) * kRowW + (kHc - 1) + L2 + s0;
+        const RingT *b1 = ring + (p1 % kRingA) * kRowW + (kHc - 1) + L2 + s1;
         const int32_t a0 = b0[0], a1 = b0[1], a2 = b0[2], a3 = b0[dd], a4 = b0[dd + 1];
         int32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
         if (NP > 1) c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
@@ -635,7 +663,7 @@ __device__ __forceinline__ void far_cells(const Z &z, uint32_t p, const int32_t 
                                           int32_t &hA, int32_t &hB, int32_t &hC, int32_t &dB, int32_t &dC)
 {
     if (!rec) {
-        pred_cells(z.lds + kLdsRing + (p % kRingA) * kRowW, sh, lane, hA, hB, hC, dB, dC);
+        pred_cells(reinterpret_cast<const RingT *>(z.lds + kLdsRing) + (p % kRingA) * kRowW, sh, lane, hA, hB, hC, dB, dC);
         return;
     }
     const int32_t i = 2 * lane + sh;
@@ -740,7 +768,7 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
     const int li = (int)(r & 63u);
     const uint32_t np = info >> 8;
     const int32_t sh = coff - S.pOff;
-    const int32_t *ring = z.lds + kLdsRing;
+    const RingT *ring = reinterpret_cast<const RingT *>(z.lds + kLdsRing);
     int32_t off;
     kind = 4;
     if (info & kInfoFar) {
@@ -864,9 +892,9 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         }
         const int32_t key = __builtin_amdgcn_readlane(rk, 63);
         // ring row, meta window
-        int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
-        row[0] = make_int2(nH0, nH1);
-        row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
+        RingT *row = reinterpret_cast<RingT *>(z.lds + kLdsRing) + ring + kHc + c.L2;
+        ring_store2(row, nH0, nH1);
+        ring_store2(row + (kDc - kHc), Dv0, Dv1);
         // (the offset / key vectors after the fast / cold join, below)
         row_key = key;
         if (cold && (info & kInfoSpill)) {
@@ -1000,7 +1028,7 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
     const int lane = lane_id();
     const int li = (int)(r & 63u);
     const uint32_t np = info >> 8;
-    const int32_t *ring = z.lds + kLdsRing;
+    const RingT *ring = reinterpret_cast<const RingT *>(z.lds + kLdsRing);
     if (info & kInfoFar) {
         int32_t o = off;
         // band placement is wave 0's; the cell tags are predecessor slots
@@ -1129,16 +1157,16 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const uint32_t np = info >> 8;
     const int32_t off = __builtin_amdgcn_readlane(vOff, li);
     const uint32_t qp = win_codes(rd_win16(z, off, z.hbm && win_has(S.wc0, S.wnc, off)), off, 0);
-    const int2 Dv = reinterpret_cast<const int2 *>(z.lds + kLdsRing + (r % kRingA) * kRowW + kDc + c.L2)[0];
+    const RingT *dv = reinterpret_cast<const RingT *>(z.lds + kLdsRing) + (r % kRingA) * kRowW + kDc + c.L2;
     PredAcc A;
-    A.Dv0 = Dv.x, A.Dv1 = Dv.y;
+    A.Dv0 = dv[0], A.Dv1 = dv[1];
     const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
     const int32_t sh = off - __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
     if (__builtin_expect(np == 1 && (uint32_t)(sh + 3) <= 7u && !(info & kInfoFar), 1)) {
         // one predecessor in the padded band: its H at t-1, t, t+1; D-ext is
         // D > H + O + E (D = max(H + O + E, D' + E))
-        const int32_t *row = z.lds + kLdsRing + (p0 % kRingA) * kRowW;
-        const int32_t *b = row + (kHc - 1) + c.L2 + sh;  // cell 2l + sh - 1
+        const RingT *row = reinterpret_cast<const RingT *>(z.lds + kLdsRing) + (p0 % kRingA) * kRowW;
+        const RingT *b = row + (kHc - 1) + c.L2 + sh;  // cell 2l + sh - 1
         // three ds_read_b32 at a 2-word lane stride: a 2-way bank conflict
         // each.  (A variant with one aligned ds_read_b64 per lane and
         // the third cell by DPP cut SQ_LDS_BANK_CONFLICT 1.54e9 -> 1.12e9
@@ -1191,7 +1219,7 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
     for (int i = lane; i < kRingA * 16; i += 64) {
         const int k = i & 15;
         const int w = k < 4 ? k : k < 8 ? kHc + kW + (k - 4) : k < 12 ? kDc - 4 + (k - 8) : kDc + kW + (k - 12);
-        z.lds[kLdsRing + (i >> 4) * kRowW + w] = k < 8 ? kNegH : kNeg;
+        reinterpret_cast<RingT *>(z.lds + kLdsRing)[(i >> 4) * kRowW + w] = ring_val(k < 8 ? kNegH : kNeg);
     }
     volatile DpJob *job = dp_job(z);
     if (z.hbm) {  // the read's first two window chunks
@@ -1360,9 +1388,9 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
             if ((uint32_t)c.L2 + 1 >= m) nH1 = kNegH;
         }
         const int32_t key = __builtin_amdgcn_readlane(rk, 63);
-        int2 *row = reinterpret_cast<int2 *>(z.lds + kLdsRing + ring + kHc + c.L2);
-        row[0] = make_int2(nH0, nH1);
-        row[(kDc - kHc) / 2] = make_int2(Dv0, Dv1);
+        RingT *row = reinterpret_cast<RingT *>(z.lds + kLdsRing) + ring + kHc + c.L2;
+        ring_store2(row, nH0, nH1);
+        ring_store2(row + (kDc - kHc), Dv0, Dv1);
         row_key = key;
         if (cold && (info & kInfoSpill)) {
             // a successor lies beyond the ring: keep this row in HBM
@@ -1463,7 +1491,7 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     for (int i = lane; i < kRingA * 16; i += 64) {
         const int k = i & 15;
         const int w = k < 4 ? k : k < 8 ? kHc + kW + (k - 4) : k < 12 ? kDc - 4 + (k - 8) : kDc + kW + (k - 12);
-        z.lds[kLdsRing + (i >> 4) * kRowW + w] = k < 8 ? kNegH : kNeg;
+        reinterpret_cast<RingT *>(z.lds + kLdsRing)[(i >> 4) * kRowW + w] = ring_val(k < 8 ? kNegH : kNeg);
     }
     if (z.hbm) {  // the read's first two window chunks
         z.wa = 0, z.wpend = false;
@@ -1578,7 +1606,9 @@ __device__ __forceinline__ unsigned long long wave_hw_id()
 __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uint32_t &ej_out)
 {
     er_out = ej_out = 0;
-    if (m >= (1u << 22)) {  // keys of the row-max scan need |H'| < 2^24
+    // keys of the row-max scan need |H'| < 2^24; the int16 ring, reads of at
+    // most kRing16MaxRead bases (the host never sends longer ones to it)
+    if (m >= (1u << 22) || (sizeof(RingT) == 2 && m > kRing16MaxRead)) {
         z.status = kErrReadLen;
         return;
     }
@@ -1600,13 +1630,20 @@ __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uin
 // offsets of the current and previous block sit in one VGPR (readlane);
 // events collect in a VGPR, lane j & 63, stored 64 at a time.
 // ----------------------------------------------------------------------------
-constexpr uint32_t kTbRows = 32;
-constexpr uint32_t kTbBufWords = kTbRows * 64;  // 32 rows x 256 B
+// rows per staged record block: 32, or 16 where the ring area is the int16
+// one (solo16: one 16-row block, 4 KiB, fits the 4,352 B area; the window
+// walk below uses lanes 0-15 of each 32-lane half then)
+#ifndef CCSX_TB_ROWS
+#define CCSX_TB_ROWS 32
+#endif
+constexpr uint32_t kTbRows = CCSX_TB_ROWS;
+static_assert(kTbRows == 32 || kTbRows == 16, "record blocks of 16 or 32 rows");
+constexpr uint32_t kTbBufWords = kTbRows * 64;  // kTbRows rows x 256 B
 // record blocks staged at once: two (the next block's DMA overlaps the walk
 // of the current one) where the DP ring area holds them, else one (the solo
 // configuration's 8-row ring: a block switch waits for its DMA, which the
 // other ZMWs resident on the SIMD cover)
-constexpr uint32_t kTbBufs = (uint32_t)(kRingA * kRowW) >= 2 * kTbBufWords + 128 ? 2u : 1u;
+constexpr uint32_t kTbBufs = (uint32_t)kRingWords >= 2 * kTbBufWords + 128 ? 2u : 1u;
 constexpr uint32_t kTbMeta = kTbBufs * kTbBufWords;  // LDS word of the blocks' row meta (64 words per buffer)
 
 // Traceback step tables indexed by (state, cell code), state 0 = H, 1 = D,
@@ -1633,7 +1670,7 @@ constexpr uint64_t tb_table(uint32_t st, bool act)
 }
 constexpr uint64_t kTbAct[3] = {tb_table(0, true), tb_table(1, true), tb_table(2, true)};
 constexpr uint64_t kTbNext[3] = {tb_table(0, false), tb_table(1, false), tb_table(2, false)};
-static_assert(kTbBufs * (kTbBufWords + 64) <= (uint32_t)(kRingA * kRowW), "traceback buffers live in the DP ring area");
+static_assert(kTbBufs * (kTbBufWords + 64) <= (uint32_t)kRingWords, "traceback buffers live in the DP ring area");
 
 // LDS-DMA of 32-row block bi into buffer buf: records (8 KB) and the row
 // meta words (band offset | far << 31); the data bypass VGPRs, so nothing in
@@ -1644,7 +1681,7 @@ __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
     const uint8_t *src = z.ws + z.L.codes + (size_t)bi * kTbRows * 256 + lane * 16u;
     int32_t *dst = z.lds + buf * kTbBufWords;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < (int)kTbRows / 4; ++k)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(src + k * 1024), dst + k * 256, 16, 0, 0);
     const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + bi * kTbRows + lane;
     __builtin_amdgcn_global_load_lds(ms, z.lds + kTbMeta + buf * 64, 4, 0, 0);
@@ -1774,11 +1811,11 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     auto enter = [&]() {
         const uint32_t mt = (uint32_t)z.lds[kTbMeta + buf * 64 + lane];
         voff = mt & 0x7FFFFFFFu;
-        vrot = (tb_rot(lane) - 2u * voff) & 255u;
-        farm = (uint32_t)ballot((mt >> 31) != 0u);
+        vrot = (tb_rot(base + lane) - 2u * voff) & 255u;  // (base: a multiple of kTbRows)
+        farm = (uint32_t)ballot((mt >> 31) != 0u) & (uint32_t)((1ull << kTbRows) - 1u);
         // lanes 32-63 take lane l - 32's rotation (v_permlane32_swap: no LDS)
         vrot32 = (uint32_t)__builtin_amdgcn_permlane32_swap(vrot, vrot, false, false)[0] - ((lane >> 5) * 4u);
-        rowb32 = (buf * 32u + (lane & 31u)) << 8;
+        rowb32 = (buf * kTbRows + (lane & (kTbRows - 1u))) << 8;
         jw = INT32_MIN / 2;
         jwn = INT32_MAX;
     };
@@ -2123,7 +2160,7 @@ __device__ __forceinline__ int merge_in_lds(uint32_t R)
 #ifdef CCSX_MERGE_NO_LDS  // measurement variant (LDS bank-conflict attribution)
     return 0 * R;
 #endif
-    constexpr uint32_t bytes = (uint32_t)(kRingA * kRowW * 4);
+    constexpr uint32_t bytes = (uint32_t)kRingWords * 4u;
     return (R + 1) * 5u + 64u <= bytes ? 2 : R + 64u <= bytes ? 1 : 0;
 }
 
@@ -2827,12 +2864,14 @@ ccsx_zmw_kernel(KArgs a)
     zmw_body<false>(a, smem);
 }
 
+#ifndef CCSX_RING16  // (solo16 takes LDS-instance slices only: ccsx_gpu.cpp stage_slot)
 __global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(CCSX_WAVES_PER_EU)))
 ccsx_zmw_kernel_hbm(KArgs a)
 {
     extern __shared__ int32_t smem[];
     zmw_body<true>(a, smem);
 }
+#endif
 
 }  // namespace CCSX_KCFG
 }  // namespace ccsx
@@ -2846,21 +2885,32 @@ extern "C" void CCSX_INFO(ccsx::KCfgInfo *o)
     o->threads = (uint32_t)K::kBlockThreads;
     o->ring_rows = (uint32_t)ccsx::kRingA;
     o->ring_back = (uint32_t)ccsx::kRing;
+    o->waves_per_simd = CCSX_WAVES_PER_EU;
+    o->max_read = sizeof(K::RingT) == 2 ? K::kRing16MaxRead : 0u;
 }
 
 extern "C" hipError_t CCSX_LAUNCH(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s)
 {
     namespace K = ccsx::CCSX_KCFG;
     if (lds_bytes < (uint32_t)K::kLdsFixed * 4u) return hipErrorInvalidValue;
+#ifdef CCSX_RING16
+    if (!a->lds_read_words) return hipErrorInvalidValue;
+    const void *f = reinterpret_cast<const void *>(&K::ccsx_zmw_kernel);
+#else
     const void *f = a->lds_read_words ? reinterpret_cast<const void *>(&K::ccsx_zmw_kernel)
                                       : reinterpret_cast<const void *>(&K::ccsx_zmw_kernel_hbm);
+#endif
     if (lds_bytes > 65536) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
         if (e != hipSuccess) return e;
     }
+#ifdef CCSX_RING16
+    hipLaunchKernelGGL(K::ccsx_zmw_kernel, dim3(a->nzmw), dim3(K::kBlockThreads), lds_bytes, s, *a);
+#else
     if (a->lds_read_words)
         hipLaunchKernelGGL(K::ccsx_zmw_kernel, dim3(a->nzmw), dim3(K::kBlockThreads), lds_bytes, s, *a);
     else
         hipLaunchKernelGGL(K::ccsx_zmw_kernel_hbm, dim3(a->nzmw), dim3(K::kBlockThreads), lds_bytes, s, *a);
+#endif
     return hipGetLastError();
 }

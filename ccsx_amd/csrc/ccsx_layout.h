@@ -51,14 +51,21 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 //    thousands of ZMWs, where resident ZMWs rather than per-ZMW latency bound
 //    the launch;
 //  * solo: one wave that also computes the decision bits, an 8-row ring and
-//    one traceback buffer -- up to 16 workgroups per CU (~10 KB of LDS each).
+//    one traceback buffer -- up to 16 workgroups per CU (~10 KB of LDS each);
+//  * solo16: the solo one with an int16 ring (exact for reads of at most
+//    16,376 bases), 16-row traceback blocks and 96 VGPRs -- up to 20
+//    workgroups per CU (~5.5 KB of LDS each); slices whose pushed reads
+//    exceed that, or whose reads live in HBM, run the solo one.
 // Each configuration's object reports its own LDS words and threads
 // (KCfgInfo), so the host never restates the build flags.
-enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1, kCfgThroughput = 2, kCfgSolo = 3, kCfgCount = 4 };
+enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1, kCfgThroughput = 2, kCfgSolo = 3, kCfgSolo16 = 4,
+                           kCfgCount = 5 };
 struct KCfgInfo {
     uint32_t lds_fixed_words;  // LDS words before the read buffer
     uint32_t threads;          // workgroup size
     uint32_t ring_rows, ring_back;
+    uint32_t waves_per_simd;   // the object's register budget (amdgpu_waves_per_eu)
+    uint32_t max_read;         // longest pushed read the object takes on the LDS instance (0: any)
 };
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch

@@ -695,6 +695,15 @@ int main(int argc, char **argv)
     // (known once the devices are counted: until then the first chunk keeps
     // growing; the sizes change only how the work is cut, never the output)
     std::atomic<size_t> chunk_first(SIZE_MAX), chunk_last(SIZE_MAX);
+    {
+        // the sizes the environment fixes hold from the first record on (the
+        // defaults depend on the device count, known once the devices open)
+        size_t cm = 0, c0 = 0;
+        if (const char *e = getenv("CCSX_CHUNK")) cm = std::max<size_t>(1024, strtoull(e, nullptr, 10));
+        if (const char *e = getenv("CCSX_CHUNK0")) c0 = std::max<size_t>(1, strtoull(e, nullptr, 10));
+        if (cm) chunk_last = cm, chunk_first = c0 ? std::min(c0, cm) : std::max<size_t>(1024, cm / 2);
+        else if (c0) chunk_first = c0;
+    }
     ReadQueue rq(1);
     std::thread reader([&]() {
         size_t chunk_size = 0;
