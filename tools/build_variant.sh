@@ -4,7 +4,8 @@
 # (after its own defines, so they override them) and to the host launcher;
 # the configurations' defines come from ccsx_amd/build.py (KCFGS).
 #   [CFGS="tput occ"] [KSRC=path/to/kernel.hip] [KSCHED="..."] tools/build_variant.sh TAG -DFOO=1 ...
-# CFGS limits the extra flags to the named configurations (default: all).
+# CFGS limits the variant to the named configurations (default: all): the
+# others reuse the product's objects (also when KSRC names another source).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TAG=$1; shift
@@ -16,6 +17,11 @@ K="/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC ${
 KOBJS=""
 while read -r NAME DEFS; do
   X=("$@")
+  if [ -n "$CFGS" ] && [[ " $CFGS " != *" $NAME "* ]] && [ -f $OBJ/ccsx_kernel_${NAME}.hip.o ]; then
+    # a configuration outside CFGS: the product's object (also with KSRC)
+    KOBJS="$KOBJS $OBJ/ccsx_kernel_${NAME}.hip.o"
+    continue
+  fi
   [ -n "$CFGS" ] && [[ " $CFGS " != *" $NAME "* ]] && X=()
   rm -f $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o
   $K $DEFS "${X[@]}" -c ${KSRC:-$C/ccsx_kernel.hip} -o $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o &

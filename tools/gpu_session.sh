@@ -19,6 +19,8 @@
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
 #   cli:N[:pipe|:fifo] CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py;
 #                      pipe: generator piped in, fifo: output through a FIFO)
+#   ingest:N           step 0 + prepare alone on N config-E ZMWs (tools/ingest_rate.sh, CPU only)
+#   n2:EZMWS           bench.py through torch.distributed.run with two ranks on the box's GPU
 #   env:NAME=VALUE     export NAME for the following steps (env:NAME= unsets it)
 #   lib:NAME           the following steps load ccsx_amd/NAME (CCSX_LIB); lib: resets
 # Environment: CCSX_LIB selects a library variant for the bench steps; CCSX_WG_PER_CU caps the
@@ -115,6 +117,15 @@ step() {
       local flag=""; [ "$k" = pipe ] && flag=--pipe; [ "$k" = fifo ] && flag=--fifo-out
       timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" $flag --out "$OUT/$tag" > "$OUT/$tag.log" 2>&1
       local rc=$?; tail -5 "$OUT/$tag.log"; return $rc ;;
+    ingest)  # ingest:N -- step 0 (one reader) + prepare rate on N config-E ZMWs from a file (CPU only)
+      timeout -k 10 900 bash tools/ingest_rate.sh "$cfg" 16 "gpurun_out/$TAG" > "$OUT/ingest_$cfg.log" 2>&1
+      local rc=$?; tail -2 "$OUT/ingest_$cfg.log"; return $rc ;;
+    n2)  # n2:EZMWS -- the driver's two-rank launch on this box (torch.distributed.run, both ranks on its GPU)
+      timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29517 bench.py --gpus 2 --steps 4 --warmup 1 --e-zmws "$cfg" --e-sample 100 \
+        --nzmw 200 --roofline-zmws 1024 --e2e-zmws 1024 \
+        --out-dir "$OUT/n2" > "$OUT/bench_n2.json" 2> "$OUT/bench_n2.err"
+      local rc=$?; cat "$OUT/bench_n2.json"; return $rc ;;
     env)  # env:NAME=VALUE -- export for the following steps (env:NAME= unsets)
       if [ -n "${cfg#*=}" ]; then export "$cfg"; else unset "${cfg%%=*}"; fi ;;
     lib)  # lib:NAME -- later steps load ccsx_amd/NAME (lib: = the product library)
