@@ -2208,8 +2208,13 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
 #endif
     // M1 (wave 0): classify every read base, number the new nodes in read order
     uint32_t K = 0;
+    // (the next 64 events are loaded while these are classified: the stores
+    // below would otherwise keep the next load behind them)
+    uint32_t ev_next = w0 && R && lane < m ? ev[lane] : 0u;
     for (uint32_t j0 = 0; w0 && j0 < m; j0 += 64) {
         const uint32_t j = j0 + lane;
+        const uint32_t ev_cur = ev_next;
+        if (R && j + 64 < m) ev_next = ev[j + 64];
         bool isnew = false;
         uint32_t pt = 0, cs = 1, fix = kNone, t = 0, bq = 0;
         if (j < m) {
@@ -2217,7 +2222,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
             if (R == 0) {
                 isnew = true;
             } else {
-                const uint32_t e = ev[j], v = e & 0x3FFFFFFFu, kind = e >> 30;
+                const uint32_t e = ev_cur, v = e & 0x3FFFFFFFu, kind = e >> 30;
                 if (kind == EV_ALN) {
                     if ((nb[v] & 3u) == bq) {
                         t = v;
@@ -2366,10 +2371,26 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
         cntn[n] = addp[n] != kNone ? 1u : 0u;
     }
     __syncthreads();
-    // (one target row per read base, so the read-modify-writes never collide)
-    for (uint32_t j = tid; j < m; j += T) {
-        const uint32_t n = newidx(tgt[j]);
-        mem2[(size_t)n * nw + (k >> 6)] |= 1ull << (k & 63u);
+    // (one target row per read base, so the read-modify-writes never collide;
+    // MB bases per thread per pass, loads first: each base's three dependent
+    // loads -- target, shift, membership word -- overlap the others', where
+    // one base per pass serialised them behind the previous pass's store)
+    {
+        const uint64_t kbit = 1ull << (k & 63u);
+        const uint32_t kw = k >> 6;
+        for (uint32_t j0 = tid; j0 < m; j0 += MB * T) {
+            uint32_t tv[MB], nn[MB];
+            uint64_t mv[MB];
+#pragma unroll
+            for (uint32_t b = 0; b < MB; ++b) tv[b] = j0 + b * T < m ? tgt[j0 + b * T] : 0u;
+#pragma unroll
+            for (uint32_t b = 0; b < MB; ++b) nn[b] = j0 + b * T < m ? newidx(tv[b]) : 0u;
+#pragma unroll
+            for (uint32_t b = 0; b < MB; ++b) mv[b] = j0 + b * T < m ? mem2[(size_t)nn[b] * nw + kw] : 0ull;
+#pragma unroll
+            for (uint32_t b = 0; b < MB; ++b)
+                if (j0 + b * T < m) mem2[(size_t)nn[b] * nw + kw] = mv[b] | kbit;
+        }
     }
     if (w0) {
         const uint32_t E2 = wave_scan_hbm<true>(cntn, poff2, R2);
@@ -2389,7 +2410,10 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     uint4 *rrec = P<uint4>(z, z.L.rrec);
     uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
     // (PB rows per thread per pass, loads first)
-    constexpr uint32_t PB = 2;
+#ifndef CCSX_MERGE_PB
+#define CCSX_MERGE_PB 2
+#endif
+    constexpr uint32_t PB = CCSX_MERGE_PB;
     for (uint32_t x0 = tid; x0 < R; x0 += PB * T) {
       uint32_t bn[PB], be0[PB], be1[PB], bad[PB], bo[PB], bq[PB][4];
 #pragma unroll
