@@ -15,6 +15,7 @@
 #   e2e:N[:KCFG]       bench.py's end-to-end line (config E, ccsx_gpu_run) on N ZMWs per GPU
 #   kt:CFG             rocprofv3 kernel-trace stats of bench --config CFG
 #   pmc:CFG            PMC passes (tools/pmc_pass.sh counter groups) over one bench step of CFG
+#   stall:LINE         SQ stall / issue / fetch counters of a bench line (B|C|D|E16k; tools/pmc_stall.sh)
 #   prof:CFG           tools/profile_gpu.sh: kernel trace of bench's timed run + PMC passes (traffic) of CFG
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
 #   cli:N[:pipe|:fifo] CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py;
@@ -105,6 +106,10 @@ step() {
         echo "kt $cfg done" ;;
     pmc)
       timeout -k 10 900 bash "$R/tools/pmc_pass.sh" "$TAG/pmc_$cfg" --config "$cfg" > "$OUT/pmc_$cfg.log" 2>&1 && echo "pmc $cfg done" ;;
+    stall)  # stall:LINE -- SQ stall / issue / fetch counters of a bench line (tools/pmc_stall.sh)
+      local d="$OUT/stall_${cfg}${CCSX_LIB:+_${CCSX_LIB%.so}}"
+      timeout -k 10 900 bash "$R/tools/pmc_stall.sh" "$d" "$cfg" > "$d.log" 2>&1; local rc=$?
+      cat "$d.log"; return $rc ;;
     prof)  # prof:CFG[:N] -- N ZMWs per GPU instead of the config's
       CFG=$cfg NZMW=$k timeout -k 10 1000 bash "$R/tools/profile_gpu.sh" "${TAG}_$cfg${k:+_n$k}" > "$OUT/prof_$cfg.log" 2>&1 && echo "prof $cfg done" ;;
     phase)  # phase:L,PASSES,N:KCFG  (per-ZMW cycle split; CCSX_LIB=libccsx_amd_diag.so for the DP detail)
