@@ -873,7 +873,7 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
 // H = kNegH, D = kNeg there, and they take no part in the row maximum.
 template <bool FULL>
 __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim, uint32_t m, const LaneK &c,
-                                        uint32_t ring)
+                                        uint32_t ring, uint32_t chn)
 {
     const int lane = lane_id();
 #ifdef CCSX_DP_STAMPS
@@ -882,10 +882,12 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
     const int li = (int)(r & 63u);
     const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
     const uint32_t base = info & 3u;
-    const int32_t coff = min(max(S.pArg + 1 - kW / 2, 0), lim);
+    // (S.pArg: the next band offset before clamping, as dpS_row's; chn: the
+    // row is a plain chain row, from the block's chain mask)
+    const int32_t coff = min(max(S.pArg, 0), lim);
     const int32_t sh = coff - S.pOff;
     // (an integer test keeps the branch scalar: a bool of && lowers to a lane mask)
-    const uint32_t fast = (uint32_t)(S.fmask >> li) & (3u >> min((uint32_t)sh, 2u)) & 1u;  // (as dpS_row)
+    const uint32_t fast = (3u >> min((uint32_t)sh, 2u)) & chn;  // (as dpS_row)
 #ifdef CCSX_DP_STAMPS
     unsigned long long ts0, ts1, ts2, ts3;
     int ckind = 0;
@@ -946,7 +948,7 @@ __device__ __forceinline__ void dpA_row(Z &z, AState &S, uint32_t r, int32_t lim
         }
         S.H0 = nH0, S.H1 = nH1, S.D0 = Dv0, S.D1 = Dv1;
         S.pOff = off;
-        S.pArg = off + 127 - (key & 127);
+        S.pArg = off + kW / 2 - (key & 127);
 #ifdef CCSX_DP_STAMPS
         if (!cold && ckind != 6) {
             ROW_STAMP(ts2);
@@ -1035,11 +1037,13 @@ __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t
     // offsets from the block's first)
     static_assert(kRingA % kBlkAB == 0, "a block's rows occupy consecutive ring slots");
     const uint32_t rb = (r0 % (uint32_t)kRingA) * (uint32_t)kRowW;
+    const uint32_t fm = (uint32_t)(S.fmask >> (r0 & 63u));  // bit i: row r0 + i is a plain chain row
     if (r0 + kBlkAB <= z.R) {
 #pragma unroll
-        for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c, rb + i * kRowW);
+        for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i)
+            dpA_row<FULL>(z, S, r0 + i, lim, m, c, rb + i * kRowW, (fm >> i) & 1u);
     } else {
-        for (uint32_t i = 0; r0 + i < z.R; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c, rb + i * kRowW);
+        for (uint32_t i = 0; r0 + i < z.R; ++i) dpA_row<FULL>(z, S, r0 + i, lim, m, c, rb + i * kRowW, (fm >> i) & 1u);
     }
     z.lds[kLdsOffRing + lane] = S.vOff;  // band offsets of the last 64 rows for the helpers
     recwin_end(S.W, r0);
