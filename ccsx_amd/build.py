@@ -42,11 +42,12 @@ KCFGS = [(n, [f"-DCCSX_KCFG={n}", f"-DCCSX_LAUNCH=ccsx_launch_zmw_{n}", f"-DCCSX
                       # one-wave workgroups (dp_solo), an 8-row ring, one traceback buffer;
                       # 8-row blocks (no barriers: only the unrolling; A/B r03u: D 363.6 -> 356.8 ms)
                       ("solo", ["-DCCSX_RINGA=8", "-DCCSX_BLK=8", "-DCCSX_RING=8", "-DCCSX_HELPERS=0",
-                                "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0"]),
-                      # the solo object with an int16 ring (exact for reads <= 16,376 bases), one 16-row
+                                "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0", "-DCCSX_PRIO_TB=1", "-DCCSX_PRIO_MG=1"]),
+                      # the solo object with an int16 ring (exact for reads <= 16,256 bases), one 16-row
                       # traceback block and 96 VGPRs: ~5.5 KB of LDS, 20 workgroups per CU
                       ("solo16", ["-DCCSX_RINGA=8", "-DCCSX_BLK=8", "-DCCSX_RING=8", "-DCCSX_HELPERS=0",
-                                  "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0", "-DCCSX_RING16", "-DCCSX_TB_ROWS=16",
+                                  "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0", "-DCCSX_PRIO_TB=1", "-DCCSX_PRIO_MG=1",
+                                  "-DCCSX_RING16", "-DCCSX_TB_ROWS=16",
                                   "-DCCSX_WAVES_PER_EU=5"])]]
 
 

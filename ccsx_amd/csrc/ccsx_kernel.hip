@@ -519,6 +519,18 @@ static_assert(kBlkAB % kHelperStep == 0, "each helper takes the same number of r
 #define CCSX_PRIO_MERGE 2
 #endif
 constexpr int kPrioWave0 = CCSX_PRIO_WAVE0, kPrioMerge = CCSX_PRIO_MERGE;
+// the one-wave objects (no helpers): issue priority of the traceback and the
+// merge over the other resident ZMWs' DP rows (s_setprio: VALU issue goes by
+// priority, then age).  1 / 1 on solo and solo16 (build.py): E16k -0.9 %, D
+// -1.4 % (r05x); 2 / 1, 2 / 2, 3 / 1 measured the same (r05w), everything but
+// the DP at 1 or 2 0.1-0.3 % behind
+#ifndef CCSX_PRIO_TB
+#define CCSX_PRIO_TB 0
+#endif
+#ifndef CCSX_PRIO_MG
+#define CCSX_PRIO_MG 0
+#endif
+constexpr int kPrioTb = CCSX_PRIO_TB, kPrioMg = CCSX_PRIO_MG;
 static_assert(kRingA >= kRing + (kHelpers ? 2 * kBlkAB : 0), "B reads predecessors up to kRing rows behind its row");
 
 
@@ -2906,7 +2918,9 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             if (z.status) return 0;
             unsigned long long t2 = pstamp();
             z.pf[kPfDp] += t2 - t1;
+            if constexpr (kHelpers == 0 && kPrioTb > 0) __builtin_amdgcn_s_setprio(kPrioTb);
             traceback(z, m, er, ej);
+            if constexpr (kHelpers == 0 && kPrioTb > 0) __builtin_amdgcn_s_setprio(0);
             if (z.status) return 0;
             t1 = pstamp();
             z.pf[kPfTrace] += t1 - t2;
@@ -2916,9 +2930,11 @@ __device__ __forceinline__ uint32_t run_poa(Z &z, uint32_t n, const uint8_t *zse
             if (lane_id() == 0) job->kind = kJobMerge, job->m = m, job->R = z.R, job->cur = (uint32_t)z.cur, job->k = k;
             __syncthreads();  // J: job posted
             const int lm = merge_in_lds(z.R);
+            if constexpr (kHelpers == 0 && kPrioMg > 0) __builtin_amdgcn_s_setprio(kPrioMg);
             if (lm == 2) merge<2>(z, k, m, threadIdx.x);
             else if (lm == 1) merge<1>(z, k, m, threadIdx.x);
             else merge<0>(z, k, m, threadIdx.x);
+            if constexpr (kHelpers == 0 && kPrioMg > 0) __builtin_amdgcn_s_setprio(0);
         }
         if (z.status) return 0;
         staged = k + 1 < z.d.n;  // (the merge staged read k + 1 under run_poa's own checks)
