@@ -360,41 +360,10 @@ typedef int16_t RingT;
 #else
 typedef int32_t RingT;
 #endif
-// (16,256 rather than 16,376: solo16's packed rows also hold X = H' + 2t,
-// t < 128, as int16 -- at most 2m + 254)
+// (16,256 rather than 16,376: round 5's packed-row variant, commit bf58425,
+// also held X = H' + 2t, t < 128, as int16 -- at most 2m + 254)
 constexpr uint32_t kRing16MaxRead = 16256;
 
-// Packed int16 pairs (the solo16 object's full-band rows): a lane's two cells
-// in one VGPR, cell t0 = 2 lane in the low half, t1 in the high half, so one
-// v_pk_* instruction does the work of two.  Adds and subtracts saturate (the
-// -inf class stays at -32768); the sign bit of a saturating difference a - b
-// (bits 15 / 31) is the comparison b > a of that half.
-typedef short pk16 __attribute__((ext_vector_type(2)));
-typedef unsigned short pku16 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ pk16 PKV(uint32_t v) { return __builtin_bit_cast(pk16, v); }
-__device__ __forceinline__ uint32_t PKW(pk16 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ uint32_t pk_adds(uint32_t a, uint32_t b) { return PKW(__builtin_elementwise_add_sat(PKV(a), PKV(b))); }
-__device__ __forceinline__ uint32_t pk_subs(uint32_t a, uint32_t b) { return PKW(__builtin_elementwise_sub_sat(PKV(a), PKV(b))); }
-__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) { return PKW(__builtin_elementwise_max(PKV(a), PKV(b))); }
-// per half: 0xFFFF where the half is negative, else 0
-__device__ __forceinline__ uint32_t pk_negmask(uint32_t a) { return PKW(PKV(a) >> (pk16){15, 15}); }
-// per half: 1 where the half is negative, else 0
-__device__ __forceinline__ uint32_t pk_negbit(uint32_t a)
-{
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, a) >> (pku16){15, 15});
-}
-// per half: v << (s & 15)
-__device__ __forceinline__ uint32_t pk_shl(uint32_t v, uint32_t s)
-{
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, v) << (__builtin_bit_cast(pku16, s) & (pku16){15, 15}));
-}
-// {lo, hi} saturated to int16 (v_cvt_pk_i16_i32)
-__device__ __forceinline__ uint32_t pk_of(int32_t lo, int32_t hi) { return PKW(__builtin_amdgcn_cvt_pk_i16(lo, hi)); }
-__device__ __forceinline__ int32_t pk_lo(uint32_t v) { return (int32_t)(int16_t)v; }
-__device__ __forceinline__ int32_t pk_hi(uint32_t v) { return (int32_t)v >> 16; }
-// v in both halves (a constant)
-__host__ __device__ constexpr uint32_t pk2(int32_t v) { return ((uint32_t)v & 0xFFFFu) * 0x10001u; }
-constexpr uint32_t kPkNeg = 0x80008000u;  // {-inf, -inf}
 // a value as the ring stores it (-inf class: -32768 in the int16 ring)
 __device__ __forceinline__ RingT ring_val(int32_t v) { return sizeof(RingT) == 2 ? (RingT)max(v, -32768) : (RingT)v; }
 // the lane's two adjacent cells (row points at cell 2 lane) of H or D
@@ -1539,163 +1508,6 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
 #endif
 }
 
-// per-lane constants of a packed row
-struct LaneP {
-    uint32_t cIP;     // {O + E t0, O + E t1}: the source term at offset 0 and the insertion start
-    uint32_t L4P;     // {2 t0, 2 t1}: X = H' + 2t
-    int32_t K0, K1;   // the row-max key from X: (X << 7) + K = (H' << 7) | (127 - t)
-};
-
-__device__ __forceinline__ LaneP lane_pconsts(const LaneK &c)
-{
-    LaneP p;
-    p.cIP = pk_of(c.cI0, c.cI1);
-    p.L4P = pk_of(c.L4, c.L4 + 2);
-    p.K0 = c.kc0 - (c.L4 << 7), p.K1 = c.kc1 - ((c.L4 + 2) << 7);
-    return p;
-}
-
-// dpS_row for the solo16 object's full-band rows (m >= W): the same values,
-// decision bits and records, with the lane's two cells as one packed int16
-// pair through the recurrence (S.H0 / S.D0 hold the packed H / D of row r - 1,
-// S.H1 / S.D1 are unused).  Exactness: every real value of the row -- H', M,
-// D, X = H' + 2t <= 2m + 254 and the source terms -- lies inside int16 for m <=
-// kRing16MaxRead; a difference or an insertion start that saturates below
-// -32768 is only ever compared with the always-real H' of its cell and loses
-// either way; the -inf class behaves as the int16 ring's (ring_val above).  The
-// insertion scan, the row-max key and the free-end candidates stay int32.
-// The match score is one shift of a 16-bit pattern: per half, the low four
-// bits of C are q + 4 q' (the cell's read code q in bits 0-1), and bit 15 of
-// (0x1111 << (3 - base)) << (q + 4 q') is set iff q == base.
-__device__ __forceinline__ void dpS_rowP(Z &z, AState &S, SolB &B, uint32_t r, int32_t lim, uint32_t m,
-                                         const LaneK &c, const LaneP &p, uint32_t ring, const RowX &x)
-{
-    const int lane = lane_id();
-    const int li = (int)(r & 63u);
-    const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.info, li);
-    const uint32_t base = info & 3u;
-    const uint32_t np = info >> 8;
-    const int32_t coff = min(max(S.pArg, 0), lim);
-    const int32_t sh = coff - S.pOff;
-    const uint32_t fast = (3u >> min((uint32_t)sh, 2u)) & x.chn;
-    const uint32_t lutP = 0x88888888u >> base;  // pk2(0x8888 >> base)
-    int32_t row_key = 0;
-    auto tail = [&](int32_t off, uint32_t qp, uint32_t MhP, uint32_t DvP, uint32_t dxw, uint32_t tagw,
-                    const PredAcc &A, bool cold) __attribute__((always_inline)) {
-        S.qn = rd_win16(z, off, z.hbm && win_has(z.wa, 2, off));
-        // the source terms {O + E j0, O + E j1} (0 at j = 0)
-        const int32_t j0 = off + c.L2;
-        const uint32_t srcP = pk_of(kO + kE * j0 - kO * (1 - min(j0, 1)), kO + kE * (j0 + 1));
-        const uint32_t Sn = pk_subs(MhP, srcP);  // sign: M from the source term
-        const uint32_t C = ((qp >> 2) << 16) | qp;
-        const uint32_t mt = pk_negmask(pk_shl(lutP, C));
-        const uint32_t score = (mt & pk2(kMs)) | (~mt & pk2(kXs));
-        const uint32_t M = pk_adds(pk_max(MhP, srcP), score);
-        const uint32_t Sd = pk_subs(M, DvP);     // sign: D beat M
-        const uint32_t hp = pk_max(M, DvP);
-        const uint32_t X = pk_adds(hp, p.L4P);
-        const int32_t X0 = pk_lo(X), X1 = pk_hi(X);
-        int32_t incl = max(X0, X1);
-        int32_t rk = max((X0 << 7) + p.K0, (X1 << 7) + p.K1);
-        wave_incl_max2(incl, rk);
-        const int32_t Pex = wave_shr1(kNeg, incl);
-        const int32_t ex1 = max(Pex, X0);
-        const uint32_t PexCI = pk_adds(pk_of(Pex, ex1), p.cIP);
-        const uint32_t nH = pk_max(PexCI, hp);
-        const uint32_t Si = pk_subs(hp, PexCI);  // sign: the insertion won
-        const int32_t key = __builtin_amdgcn_readlane(rk, 63);
-        uint32_t *row = reinterpret_cast<uint32_t *>(reinterpret_cast<RingT *>(z.lds + kLdsRing) + ring + kHc + c.L2);
-        row[0] = nH;
-        row[(kDc - kHc) / 2] = DvP;
-        row_key = key;
-        if (cold && (info & kInfoSpill)) {
-            const uint32_t sl = S.nspill++;
-            if (sl < z.d.scap) {
-                int32_t *rec = reinterpret_cast<int32_t *>(z.ws + z.L.spill + (size_t)sl * kSpillRec);
-                reinterpret_cast<int2 *>(rec)[lane] = make_int2(pk_lo(nH), pk_hi(nH));
-                reinterpret_cast<int2 *>(rec + kW)[lane] = make_int2(pk_lo(DvP), pk_hi(DvP));
-                if (lane == 0) rec[256] = off, rec[257] = key, P<uint32_t>(z, z.L.sslot)[r] = sl;
-            } else {
-                z.status = kErrSpill;
-            }
-        }
-        S.H0 = (int32_t)nH, S.D0 = (int32_t)DvP;
-        S.pOff = off;
-        S.pArg = off + kW / 2 - (key & 127);
-        // the record: code = i ? INS : d ? DEL : mp ? MPRED : MSRC per half
-        const int32_t X1L = wave_shr1(INT32_MAX, X1);
-        const uint32_t iew = (Pex > X1L ? 8u : 0u) | (Pex > X0 ? 0x80000u : 0u);
-        const uint32_t Mi = pk_negmask(Si), Md = pk_negmask(Sd);
-        static_assert(HC_MPRED == 0 && HC_MSRC == 1 && HC_DEL == 2 && HC_INS == 3, "code bits");
-        const uint32_t hd = (Md & pk2(HC_DEL)) | (~Md & pk_negbit(Sn));
-        const uint32_t hc = (Mi & pk2(HC_INS)) | (~Mi & hd);
-        const uint32_t w = hc | dxw | iew | tagw;
-        if (cold && __builtin_expect(np > 63u, 0)) {
-            reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
-                make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
-        }
-        const int32_t eb = (off << 1) + x.em1;
-        const int32_t e0 = X0 + eb;
-        int32_t e1 = X1 + eb;
-        if (__builtin_expect(off == lim, 0)) e1 = writelane(e1, __builtin_amdgcn_readlane(e1, 63) + 3, 63);
-        const bool c1 = e1 > e0;
-        const int32_t e01 = c1 ? e1 : e0;
-        if (e01 > B.bE) B.bE = e01, B.bKey = r * 2 + (c1 ? 1u : 0u);
-        __builtin_amdgcn_raw_buffer_store_b32(w, B.rc, (((uint32_t)lane * 4u + x.rot) & 255u) + x.ioff, x.sbase, 0);
-    };
-    const uint32_t SH = (uint32_t)S.H0, SD = (uint32_t)S.D0;
-    if (__builtin_expect(fast, 1)) {
-        PredAcc A;
-        constexpr uint32_t kTagFast = pk2((1 << 4) | (1 << 10));  // M / D tag 1: row r - 1
-        if (sh == 0) {
-            const uint32_t MhP = __builtin_amdgcn_alignbit(SH, (uint32_t)wave_shr1((int)kPkNeg, (int)SH), 16);
-            const uint32_t a = pk_adds(SH, pk2(kO + kE)), b = pk_adds(SD, pk2(kE));
-            tail(coff, win_codes(S.qn, S.pOff, 0), MhP, pk_max(a, b), (pk_subs(a, b) >> 13) & 0x40004u, kTagFast, A,
-                 false);
-        } else {
-            const uint32_t ha = __builtin_amdgcn_alignbit((uint32_t)wave_shl1((int)kPkNeg, (int)SH), SH, 16);
-            const uint32_t da = __builtin_amdgcn_alignbit((uint32_t)wave_shl1((int)kPkNeg, (int)SD), SD, 16);
-            const uint32_t a = pk_adds(ha, pk2(kO + kE)), b = pk_adds(da, pk2(kE));
-            tail(coff, win_codes(S.qn, S.pOff, 1), SH, pk_max(a, b), (pk_subs(a, b) >> 13) & 0x40004u, kTagFast, A,
-                 false);
-        }
-    } else {
-        // the cold paths take the unpacked cells
-        AState U = S;
-        U.H0 = pk_lo(SH), U.H1 = pk_hi(SH), U.D0 = pk_lo(SD), U.D1 = pk_hi(SD);
-        PredAcc A;
-        int32_t off;
-        int kind;
-        dpA_cold<true>(z, U, r, info, coff, lim, off, A, kind);
-        (void)kind;
-        const uint32_t d = (uint32_t)(off - S.pOff);
-        const uint32_t qp = d <= 3u ? win_codes(S.qn, S.pOff, (int32_t)d)
-                                    : win_codes(rd_win16(z, off, z.hbm && win_has(z.wa, 2, off)), off, 0);
-        const uint32_t tagw = (((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10)) |
-                              ((((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10)) << 16);
-        tail(off, qp, pk_of(A.Mh0, A.Mh1), pk_of(A.Dv0, A.Dv1), A.dx0 | (A.dx1 << 16), tagw, A, true);
-    }
-    S.vOff = writelane(S.vOff, S.pOff, li);
-    S.vKey = writelane(S.vKey, row_key, li);
-}
-
-// the solo16 object's full-band rows may take the packed row (CCSX_PACKED_ROWS:
-// measured neutral to 2.5 % slower on E16k, r05j / r05k -- a variant)
-#if defined(CCSX_RING16) && defined(CCSX_PACKED_ROWS)
-constexpr bool kPackedRows = true;
-#define PC pc
-#else
-constexpr bool kPackedRows = false;
-#define PC 0
-#endif
-template <bool FULL, class PCT>
-__device__ __forceinline__ void dpS_any(Z &z, AState &S, SolB &B, uint32_t r, int32_t lim, uint32_t m, const LaneK &c,
-                                        const PCT &pc, uint32_t ring, const RowX &x)
-{
-    if constexpr (FULL && kPackedRows) dpS_rowP(z, S, B, r, lim, m, c, pc, ring, x);
-    else dpS_row<FULL>(z, S, B, r, lim, m, c, ring, x);
-}
-
 // rows [r0, r0 + kBlkAB) and, per 16-row group, the row meta words {band
 // offset | far << 31} the traceback reads (helper 0's job in dpB_block)
 template <bool FULL>
@@ -1705,9 +1517,6 @@ __device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0,
     const uint32_t R = z.R;
     const int32_t lim = FULL ? (int32_t)m - kW : 0;
     const LaneK c = lane_consts(lane);
-#if defined(CCSX_RING16) && defined(CCSX_PACKED_ROWS)
-    const LaneP pc = lane_pconsts(c);
-#endif
     recwin_begin(z, S.W, r0);
     if ((r0 & 63u) == 0) {
         const uint32_t inf = S.W.cur.info;
@@ -1724,11 +1533,11 @@ __device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0,
     if (r0 + kBlkAB <= R) {
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i)
-            dpS_any<FULL>(z, S, B, r0 + i, lim, m, c, PC, rb + i * kRowW,
+            dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + i * kRowW,
                           RowX{(fm >> i) & 1u, rot0 + 8u * i, 256u * i, r0 * 256u, em1});
     } else {
         for (uint32_t i = 0; r0 + i < R; ++i)
-            dpS_any<FULL>(z, S, B, r0 + i, lim, m, c, PC, rb + i * kRowW,
+            dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + i * kRowW,
                           RowX{(fm >> i) & 1u, rot0 + 8u * i, 256u * i, r0 * 256u, em1});
     }
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
@@ -1757,7 +1566,6 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     }
     AState S;
     S.H0 = S.H1 = kNegH, S.D0 = S.D1 = kNeg;
-    if (FULL && kPackedRows) S.H0 = S.D0 = (int32_t)kPkNeg;  // (dpS_rowP's packed pairs)
     S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
     S.qn = rd_win16(z, 0, true);
     S.nspill = 0;
@@ -2066,38 +1874,6 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     // the window below it (columns [jw - 8, jw - 4)), valid while jwn == jw
     uint32_t wnx = 0;
     int32_t jwn = INT32_MAX;
-    // (one staged buffer, 16-row blocks: solo16) the block below the staged
-    // one, loaded into 17 VGPRs -- free in this phase -- while the staged block
-    // is walked; a switch to it writes them to the LDS buffer (five ds_writes,
-    // ordered after the walk's reads of the old block) instead of waiting for
-    // an HBM round trip.  Buffer loads: a flat load would count in lgkmcnt
-    // and hold up every LDS wait of the walk.
-#ifdef CCSX_TB_VPF  // (a variant: 2.7 % slower on E16k, r05n)
-    constexpr bool kVpf = kTbBufs == 1 && kTbRows == 16;
-#else
-    constexpr bool kVpf = false;
-#endif
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 pfd[kTbRows / 4];
-    uint32_t pfm = 0, pfb = ~0u;
-    const auto rcodes = brsrc(z.ws + z.L.codes, z.R * 256u);
-    const auto rmeta = brsrc(z.ws + z.L.rmeta, z.R * 4u);
-    auto tb_pf = [&](uint32_t b) {
-#pragma unroll
-        for (uint32_t k = 0; k < kTbRows / 4; ++k)
-            pfd[k] = __builtin_amdgcn_raw_buffer_load_b128(rcodes, b * (kTbRows * 256u) + lane * 16u + k * 1024u, 0, 0);
-        // (rows past R: out of the buffer's range, zeros)
-        pfm = __builtin_amdgcn_raw_buffer_load_b32(rmeta, lane < kTbRows ? (b * kTbRows + lane) * 4u : ~0u, 0, 0);
-        pfb = b;
-    };
-    auto tb_pf_put = [&]() {
-        typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-        typedef __attribute__((address_space(3))) uint32_t lds_u32;
-        static_assert(kLdsRing == 0, "buffer 0 at LDS address 0");
-#pragma unroll
-        for (uint32_t k = 0; k < kTbRows / 4; ++k) *(lds_u32x4 *)(uintptr_t)((k * 256u + lane * 4u) * 4u) = pfd[k];
-        *(lds_u32 *)(uintptr_t)((kTbMeta + lane) * 4u) = pfm;
-    };
     auto enter = [&]() {
         const uint32_t mt = (uint32_t)z.lds[kTbMeta + buf * 64 + lane];
         voff = mt & 0x7FFFFFFFu;
@@ -2113,7 +1889,6 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     __builtin_amdgcn_s_waitcnt(0);
     enter();
     if (kTbBufs == 2 && bi) tb_dma(z, bi - 1, buf ^ 1u);
-    if (kVpf && bi) tb_pf(bi - 1);
     const auto rev = brsrc(ev, m * 4);
     uint32_t vev = 0;                      // events of bases [chunk, chunk + 64), lane = base & 63
     int32_t chunk = j & ~63;
@@ -2148,16 +1923,14 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
 #endif
         const uint32_t nb = r / kTbRows;
         if (kTbBufs == 1) {
-            if (kVpf && nb == pfb) {
-                tb_pf_put();  // the block below, from registers
-            } else {
-                // one buffer: the walk's LDS reads of the old block complete,
-                // then the new block's DMA.  (An L2 prefetch of the block below,
-                // one load per 128 B line on entering a block, measured +1.9 %
-                // on config D: A/B r03o)
-                __builtin_amdgcn_s_waitcnt(0);
-                tb_dma(z, nb, 0u);
-            }
+            // one buffer: the walk's LDS reads of the old block complete,
+            // then the new block's DMA.  (An L2 prefetch of the block below,
+            // one load per 128 B line on entering a block, measured +1.9 %
+            // on config D: A/B r03o; the block below held in 17 VGPRs and
+            // written to LDS at the switch, +2.7 % on E16k with the
+            // traceback's cycles unchanged: r05n / r05o, commit bf58425)
+            __builtin_amdgcn_s_waitcnt(0);
+            tb_dma(z, nb, 0u);
         } else {
             if (nb + 1 != bi) {
                 __builtin_amdgcn_s_waitcnt(0);
@@ -2175,10 +1948,6 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             pend = -1;
         }
         if (kTbBufs == 2 && bi) tb_dma(z, bi - 1, buf ^ 1u);
-        if (kVpf) {
-            if (bi) tb_pf(bi - 1);
-            else pfb = ~0u;
-        }
 #ifdef CCSX_TB_COUNTING
         const unsigned long long ts1 = stamp();
         z.pf[kPfTbSwitch] += ts1 - ts0;

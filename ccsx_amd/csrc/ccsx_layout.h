@@ -53,7 +53,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 //  * solo: one wave that also computes the decision bits, an 8-row ring and
 //    one traceback buffer -- up to 16 workgroups per CU (~10 KB of LDS each);
 //  * solo16: the solo one with an int16 ring (exact for reads of at most
-//    16,376 bases), 16-row traceback blocks and 96 VGPRs -- up to 20
+//    16,256 bases), 16-row traceback blocks and 96 VGPRs -- up to 20
 //    workgroups per CU (~5.5 KB of LDS each); slices whose pushed reads
 //    exceed that, or whose reads live in HBM, run the solo one.
 // Each configuration's object reports its own LDS words and threads

@@ -321,7 +321,7 @@ def test_throughput_config_parity(engine, mode, cfg):
     its own decision bits) and solo16 (int16 ring) configurations, whose rings
     read back 8 rows (more rows take the far / spill path), forced on the
     parity shapes: config B/C/D-like ZMWs, wide graphs, short reads and the
-    edge cases.  (-P pushes the 20 kb segments whole: beyond solo16's 16,376
+    edge cases.  (-P pushes the 20 kb segments whole: beyond solo16's 16,256
     bases, so that call runs the solo object.)"""
     cases = edge_cases()
     zs = [synth(7600 + h, L, p) for h, (L, p) in enumerate([(10000, 8), (2000, 30), (20000, 5), (1500, 70), (60, 12)])]
@@ -353,6 +353,30 @@ def test_solo_config_hbm_read_instance(engine, mode):
     engine.set_kernel_cfg(3)
     try:
         _check(engine, zs, mode)
+        assert engine.kernel_cfg() == 3
+    finally:
+        engine.set_kernel_cfg(-1)
+
+
+def test_solo16_int16_bound(engine):
+    """solo16's int16 cells at the object's read-length limit: -P pushes the
+    segments whole, 16,256 bases each (kRing16MaxRead), identical or with
+    substitutions only, so H' climbs to ~2m and X = H' + 2t to within a few
+    units of 2m + 254 = 32,766 -- the bound the int16 recurrence is exact
+    under; then 16,257-base segments, which the host sends to
+    the int32 solo object instead (stage_slot's max_read)."""
+    import random
+    from tests.zmw_cases import mutate
+    rnd = random.Random(16256)
+    ins = bytes(rnd.choice(b"ACGT") for _ in range(16256))
+    subs = lambda: mutate(rnd, ins, 0.0, 0.0, 0.003)  # noqa: E731  (length kept)
+    zs = [raw([ins] * 3), raw([subs() for _ in range(4)])]
+    engine.set_kernel_cfg(4)
+    try:
+        _check(engine, zs, cx.MODE_PRIMITIVE)
+        assert engine.kernel_cfg() == 4
+        longer = ins + b"A"
+        _check(engine, [raw([longer] * 3)], cx.MODE_PRIMITIVE)
         assert engine.kernel_cfg() == 3
     finally:
         engine.set_kernel_cfg(-1)
