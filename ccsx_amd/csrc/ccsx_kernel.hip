@@ -1016,7 +1016,7 @@ __device__ __forceinline__ void dpA_block(Z &z, AState &S, uint32_t r0, uint32_t
     // ring slots of the block's rows: r0 is a multiple of kBlkAB, which
     // divides kRingA, so the block's rows take consecutive slots (constant
     // offsets from the block's first)
-    static_assert(kRingA % kBlkAB == 0, "a block's rows occupy consecutive ring slots");
+    static_assert(kHelpers == 0 || kRingA % kBlkAB == 0, "a block's rows occupy consecutive ring slots");  // (the solo objects run dpS_block)
     const uint32_t rb = (r0 % (uint32_t)kRingA) * (uint32_t)kRowW;
     const uint32_t fm = (uint32_t)(S.fmask >> (r0 & 63u));  // bit i: row r0 + i is a plain chain row
     if (r0 + kBlkAB <= z.R) {
@@ -1522,22 +1522,24 @@ __device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0,
         const uint32_t inf = S.W.cur.info;
         S.fmask = ballot((inf & (kInfoChain | kInfoFar | kInfoSpill)) == kInfoChain);
     }
-    static_assert(kRingA % kBlkAB == 0, "a block's rows occupy consecutive ring slots");
+    // the rows' ring slots: consecutive from r0's (kBlkAB divides kRingA), or
+    // (a block of several ring lengths, r0 a multiple of kRingA) i mod kRingA
+    static_assert(kRingA % kBlkAB == 0 || kBlkAB % kRingA == 0, "a block's rows take constant ring slots");
     const uint32_t rb = (r0 % (uint32_t)kRingA) * (uint32_t)kRowW;
     // per row of the block: bit i of fm = row r0 + i is a plain chain row;
-    // tb_rot(r0 + i) = tb_rot(r0) + 8 i (r0 is a multiple of 8)
-    static_assert(kBlkAB <= 8 && 32 % kBlkAB == 0, "a block's rows share tb_rot's 32-row period");
+    // tb_rot(r0 + i) = tb_rot(r0) + 8 i (r0 is a multiple of kBlkAB)
+    static_assert(kBlkAB <= 16 && 32 % kBlkAB == 0, "a block's rows share tb_rot's 32-row period");
     const uint32_t fm = (uint32_t)(S.fmask >> (r0 & 63u));
     const uint32_t rot0 = tb_rot(r0);
     const int32_t em1 = -2 * (int32_t)m - 1;
     if (r0 + kBlkAB <= R) {
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i)
-            dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + i * kRowW,
+            dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + (i % (uint32_t)kRingA) * kRowW,
                           RowX{(fm >> i) & 1u, rot0 + 8u * i, 256u * i, r0 * 256u, em1});
     } else {
         for (uint32_t i = 0; r0 + i < R; ++i)
-            dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + i * kRowW,
+            dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + (i % (uint32_t)kRingA) * kRowW,
                           RowX{(fm >> i) & 1u, rot0 + 8u * i, 256u * i, r0 * 256u, em1});
     }
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
