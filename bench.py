@@ -740,7 +740,12 @@ def main():
                 parts = [None] * world
                 dist.all_gather_object(parts, part)
                 if rank == 0:
-                    one = one_process_line(args, world, parts, cli["sample_holes"], args.out_dir, tmp)
+                    # (a failure here is reported in the line, never fatal: the
+                    # other ranks wait at the barrier and the headline stands)
+                    try:
+                        one = one_process_line(args, world, parts, cli["sample_holes"], args.out_dir, tmp)
+                    except Exception as e:  # noqa: BLE001
+                        one = {"zmws": args.e_zmws, "ngpu": world, "error": f"{type(e).__name__}: {e}"[:400]}
                 dist.barrier()
         finally:
             shutil.rmtree(tmp, ignore_errors=True)
