@@ -2365,7 +2365,10 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     // (MB read bases per thread per pass: their dependent loads are issued
     // together so the HBM round trips overlap)
     // (8 per thread on the solo object's 64 threads measured -0.25 %: noise, r03u)
-    constexpr uint32_t MB = 4;
+#ifndef CCSX_MERGE_MB
+#define CCSX_MERGE_MB 4
+#endif
+    constexpr uint32_t MB = CCSX_MERGE_MB;
     for (uint32_t j0 = 1 + tid; j0 < m; j0 += MB * T) {
         uint32_t sv[MB], dv[MB], e0[MB], e1[MB], p0[MB], p1[MB];
 #pragma unroll
