@@ -307,6 +307,34 @@ def cli_cells(log_path: str) -> int:
     return 0
 
 
+def cli_timeline(log_path: str) -> dict:
+    """The CLI's CCSX_TIMING log as a timeline (ms from main): device contexts
+    open, first batch started, last batch ended, output done, and the batches'
+    ZMWs per second between the first start and the last end."""
+    t = {}
+    first, last, nz = None, None, 0
+    try:
+        with open(log_path) as f:
+            for line in f:
+                if "device context(s) open at " in line:
+                    t["open_ms"] = float(line.split("open at ")[1].split()[0])
+                elif " batch of " in line and " ZMWs on context " in line:
+                    a, b = line.rsplit(": ", 1)[1].split(" ms")[0].split("-")
+                    a, b = float(a), float(b)
+                    first = a if first is None else min(first, a)
+                    last = b if last is None else max(last, b)
+                    nz += int(line.split(" batch of ")[1].split()[0])
+                elif "output done at " in line:
+                    t["output_done_ms"] = float(line.split("output done at ")[1].split()[0].rstrip(";"))
+    except OSError:
+        return t
+    if first is not None:
+        t["first_batch_ms"], t["last_batch_end_ms"], t["batched_zmws"] = first, last, nz
+        if last > first:
+            t["batch_rate_zmws_per_s"] = round(nz / ((last - first) / 1e3), 1)
+    return t
+
+
 E_BYTES_PER_ZMW = 132e3 * 1.15  # config-E FASTA bytes per ZMW, with a margin (65.7 GB per 500k)
 
 
@@ -384,6 +412,7 @@ def cli_line(args, rank: int, world: int, local: int, local_world: int, ndev: in
         res["records_in_input_order"] = scan["in_order"]
         res["output_bytes"] = scan["bytes"]
         res["cells"] = cli_cells(log)
+        res["timeline"] = cli_timeline(log)
         res["sample_holes"] = sample
         res["sample_got"] = scan["got"]
     except BaseException:
@@ -417,7 +446,33 @@ def concat_parts(parts, dst: str) -> None:
             os.remove(p)
 
 
-def one_process_line(args, world: int, parts, sample, out_dir: str, tmp: str):
+def wait_device_memory(devices, frac: float = 0.95, timeout: float = 120.0) -> dict:
+    """Untimed: wait until each device has `frac` of its memory free again
+    (the rank CLIs that just exited held most of it, and the driver clears
+    it for seconds after: VERDICT r5 weak 7, 6.4 s of a 7.68 s one-process
+    line was its device open waiting on that).  Polled in a short-lived
+    child process (tools/mem_wait.py), never by re-exec."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "mem_wait.py"), "--devices",
+           ",".join(str(d) for d in devices), "--frac", str(frac), "--timeout", str(timeout)]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout + 60)
+        out = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else {}
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
+        out = {}
+    out.setdefault("ok", False)
+    out["mem_wait_s"] = round(time.perf_counter() - t0, 3)
+    return out
+
+
+def one_process_devices(world: int, ndev: int):
+    """The devices the one-process CLI (CCSX_NGPU=world) opens: its context
+    groups go to devices g % ndev."""
+    return sorted({g % max(1, ndev) for g in range(world)})
+
+
+def one_process_line(args, world: int, parts, sample, out_dir: str, tmp: str, local_world: int | None = None,
+                     ndev: int = 1):
     """N > 1, rank 0: the whole config-E input (the ranks' inputs concatenated
     in hole order) through ONE ccsx process driving all N GPUs (CCSX_NGPU=N:
     the CLI's host-side dispatch of micro-batches to per-GPU contexts and its
@@ -427,6 +482,11 @@ def one_process_line(args, world: int, parts, sample, out_dir: str, tmp: str):
     for the oracle comparison."""
     share, _, _ = cpu_share()
     res = {"zmws": args.e_zmws, "jobs": share, "ngpu": world}
+    if local_world is not None and local_world != world:
+        # the ranks' inputs are files on their own nodes: one process on rank
+        # 0's node cannot read them (ADVICE r5)
+        res["skipped"] = f"multi-node job ({world} ranks, {local_world} on this node): the one-process line is single-node"
+        return res
     if any(p is None for p in parts):
         res["skipped"] = "a rank streamed its input from a generator pipe (no disk room for the inputs)"
         return res
@@ -441,13 +501,18 @@ def one_process_line(args, world: int, parts, sample, out_dir: str, tmp: str):
     res["input_bytes"] = os.path.getsize(full)
     env = dict(os.environ, CCSX_NGPU=str(world), CCSX_TIMING="1")
     log = os.path.join(out_dir, "cli_one_process.log")
+    # untimed, outside cli_s: the memory the rank CLIs just released
+    mw = wait_device_memory(one_process_devices(world, ndev))
+    res["mem_wait_s"] = mw["mem_wait_s"]
+    res["mem_free_frac"] = mw.get("free_frac")
+    res["mem_wait_ok"] = mw["ok"]
     try:
         dt, scan = run_cli(full, args.e_zmws, set(sample), env, share, log)
     finally:
         os.remove(full)
     res.update({"cli_s": round(dt, 3), "value": round(args.e_zmws / dt, 3), "unit": "ZMWs/s",
                 "records": scan["nrec"], "records_in_input_order": scan["in_order"], "cells": cli_cells(log),
-                "sample_got": scan["got"]})
+                "timeline": cli_timeline(log), "sample_got": scan["got"]})
     return res
 
 
@@ -461,8 +526,8 @@ def oracle_check(pairs, threads: int):
 
 def cpu_baseline(sample_holes, sample_got, threads: int | None = None, sample_j1: int = 60, timed: bool = True,
                  others=None):
-    """The CPU leg: oracle/ccsx_cpu (the product's ingest + ccs_prepare around
-    the oracle's scalar POA, ccsx's chunked pipeline, -j threads with kt_for's
+    """The CPU leg: oracle/ccsx_cpu (the product's ingest around the oracle's
+    own ccs_prepare and scalar POA, ccsx's chunked pipeline, -j threads with kt_for's
     dynamic sharing) -- a stand-in for `ccsx -A -j N`, unbuildable here
     (bsalign is not vendored): a scalar C restatement, not bsalign's SIMD code.
     On the same workload as the headline: the sampled config-E holes as a
@@ -603,14 +668,44 @@ def e2e_line(eng, batch, n: int, dist, keep):
                         "prepared push lists in host memory (ingest timed separately: tools/ingest_bench)"}, kept
 
 
-def load_traffic(cfg_key: str):
-    p = os.path.join(ROOT, "profiles", "traffic.json")
+def load_traffic(cfg_key: str, path: str | None = None):
+    p = path or os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(p) as f:
             t = json.load(f)
         return t.get(cfg_key)
     except (OSError, ValueError):
         return None
+
+
+def traffic_key(config: str | None, nzmw: int = 0, roofline_zmws: int = 0) -> str:
+    """profiles/traffic.json key of the workload a line launched: the
+    roofline line's config-E launch size (E16384), or the kernel line's
+    config, with its ZMW count when --nzmw overrides it (B_n200)."""
+    if roofline_zmws:
+        return f"E{roofline_zmws}"
+    return f"{config}_n{nzmw}" if nzmw else str(config)
+
+
+def traffic_entry(key: str, cells_per_launch: int, path: str | None = None):
+    """The PMC traffic of exactly this workload (None when no profile of it
+    exists -- never another workload's), with the algorithmic bytes beside
+    it: 2 bits of traceback per DP cell, written by the DP and read back by
+    the traceback (north_star's 2-bit traceback matrices), so the ratio says
+    how far the HBM traffic is above that."""
+    t = load_traffic(key, path)
+    if t is None:
+        return None
+    out = dict(t, key=key)
+    if t.get("cells_per_launch") is not None:
+        out["cells_match"] = int(t["cells_per_launch"]) == int(cells_per_launch)
+        if not out["cells_match"]:
+            return None  # the profile measured a different workload under this key
+    alg = cells_per_launch * 2 * 2 / 8
+    out["algorithmic_bytes"] = alg
+    if alg and t.get("bytes_per_launch"):
+        out["traffic_over_algorithmic"] = round(t["bytes_per_launch"] / alg, 2)
+    return out
 
 
 def main():
@@ -688,7 +783,7 @@ def main():
     kline = None
     if zs is not None:
         kline = kernel_line(eng, cfg, zs, args.steps, args.warmup, dist)
-        kline["traffic"] = load_traffic(args.config)
+        kline["traffic"] = traffic_entry(traffic_key(args.config, args.nzmw), kline["cells_per_step"])
         kline["workload"] = cfg["workload"]
     # the dominant kernel of the headline workload: config-E ZMWs per launch,
     # inputs resident (the solo object at this size)
@@ -712,7 +807,8 @@ def main():
         rline = {"bound": "valu-int32", "achieved": round(achieved, 4), "peak": round(VALU_PEAK_TOPS, 2),
                  "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 5),
                  "frac_vs_packed_int16": round(achieved / (2 * VALU_PEAK_TOPS), 5),
-                 "traffic": load_traffic("E16384"), "kernel": "ccsx_zmw_kernel", "kernel_cfg": eng.kernel_cfg(),
+                 "traffic": traffic_entry(traffic_key(None, roofline_zmws=args.roofline_zmws), cells),
+                 "kernel": "ccsx_zmw_kernel", "kernel_cfg": eng.kernel_cfg(),
                  "avg_launch_ms": round(avg * 1e3, 3), "launches": rsteps, "ops_per_cell": OPS_PER_CELL,
                  "cells_per_launch": int(cells), "zmws_per_launch": ecfg["nzmw"],
                  "zmws_per_s_per_launch": round(ecfg["nzmw"] / avg, 3),
@@ -743,7 +839,8 @@ def main():
                     # (a failure here is reported in the line, never fatal: the
                     # other ranks wait at the barrier and the headline stands)
                     try:
-                        one = one_process_line(args, world, parts, cli["sample_holes"], args.out_dir, tmp)
+                        one = one_process_line(args, world, parts, cli["sample_holes"], args.out_dir, tmp,
+                                               local_world=local_world, ndev=ndev)
                     except Exception as e:  # noqa: BLE001
                         one = {"zmws": args.e_zmws, "ngpu": world, "error": f"{type(e).__name__}: {e}"[:400]}
                 dist.barrier()

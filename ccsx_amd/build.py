@@ -136,9 +136,11 @@ def build_product(verbose: bool = False) -> str:
         dobjs.append(dobj)
         if _stale(dobj, [srcs[0]] + khdrs):
             # the stamps' counters need registers: 2 waves per SIMD (occupancy
-            # is not what this build measures; per-ZMW cycle counts are)
-            jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2"]
-                        + common + kflags + defs + ["-c", srcs[0], "-o", dobj])
+            # is not what this build measures; per-ZMW cycle counts are).  The
+            # diagnostic flags come after the configuration's defines, so its
+            # waves-per-EU wins over solo16's 5
+            jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + defs
+                        + ["-Wno-macro-redefined", "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2", "-c", srcs[0], "-o", dobj])
     _run_all(jobs, verbose)
     if _stale(LIB, objs):
         cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lpthread"]
@@ -177,8 +179,9 @@ def build_oracle(verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
-    # the CPU-only ccsx of bench.py's cpu_baseline leg: the product's host
-    # C-ABI (ingest, ccs_prepare) around the oracle POA
+    # the CPU-only ccsx of bench.py's cpu_baseline leg: the product's ingest
+    # (pinned by the reference's seqio.h fixtures) around the oracle's own
+    # ccs_prepare (prep_oracle.c) and POA
     cpu = os.path.join(ORACLE_DIR, "ccsx_cpu")
     csrc = os.path.join(ORACLE_DIR, "ccsx_cpu.c")
     if os.path.exists(LIB) and _stale(cpu, [csrc, LIB] + srcs + hdrs):

@@ -237,6 +237,11 @@ struct ccsx_ctx {
     bool shred_caps = false;           // tight caps sized for shredding windows (ccsx_gpu_run, shredded mode)
     uint32_t mem_share = 1;            // contexts sharing the device concurrently
     float mem_frac = 0.5f;             // of the device memory, the contexts sharing it use at most this fraction
+    // a slice staged while another process or context still holds device
+    // memory it is about to release waits up to this long for it
+    // (ccsx_gpu_set_mem_wait) before the call fails
+    uint32_t mem_wait_ms = 60000;
+    uint64_t mem_waits = 0, mem_replans = 0;  // slices that waited for memory / were cut below the plan
     bool prealloc = false;             // reserve the slice budget up front
     bool bp_log = false;               // record the -v >= 3 breakpoint log (main.c:619-620)
     std::vector<uint32_t> run_bp;      // ccsx_gpu_run: the gathered logs, (i, ncols) pairs
@@ -400,6 +405,44 @@ static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, const ccsx_ctx *c, u
     return ccsx::align256(L.total) + hi + d.outcap + uint64_t(zi.nseg) * 8 + sizeof(ccsx::ZmwDesc) + 32;
 }
 
+// The bytes a slice staged into slot s may need now: the device's free memory
+// plus what s's arenas already hold, less a 1 GB margin (stage_slot's test).
+// A context's slice plan (plan_slots) comes from its share of the device, but
+// a neighbour -- another context, or a process that just exited and whose
+// memory the driver is still clearing -- may hold part of that share for a
+// while (a rank's call failed with 28.2 GB needed, 25.7 GB free).
+static int slot_avail(ccsx_ctx *c, const Slot &s, uint64_t &avail)
+{
+    size_t freeb = 0, totb = 0;
+    HIPCHK(c, hipMemGetInfo(&freeb, &totb));
+    const uint64_t have = freeb + s.d_ws.cap + s.d_seq.cap + s.d_out.cap + s.d_msa.cap;
+    avail = have > (1ull << 30) ? have - (1ull << 30) : 0;
+    return 0;
+}
+
+// Wait (polling, up to c->mem_wait_ms) until a slice of `need` bytes fits
+// slot s; `fits` tells whether it does.
+static int wait_slot_mem(ccsx_ctx *c, const Slot &s, uint64_t need, bool &fits)
+{
+    uint64_t avail = 0;
+    int r = slot_avail(c, s, avail);
+    if (r) return r;
+    fits = need <= avail;
+    if (fits) return 0;
+    ++c->mem_waits;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!fits && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(c->mem_wait_ms)) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        if ((r = slot_avail(c, s, avail))) return r;
+        fits = need <= avail;
+    }
+    if (getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING")))
+        fprintf(stderr, "[ccsx_gpu_run] dev %d: waited %.0f ms for %.1f GB of device memory (%s)\n", c->device,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), need / 1e9,
+                fits ? "free" : "timed out");
+    return 0;
+}
+
 // Stage a slice into slot s: sizes, device buffers, the host packing of the
 // sequence arena, and the H2D copies enqueued on the slot's stream (the host
 // copies they read stay in the slot until its next stage, which follows the
@@ -496,16 +539,23 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
             if (!s.lds_read_words || (mr && pushed > mr)) s.cfg = ccsx::kCfgSolo;
         }
     }
-    size_t freeb = 0, totb = 0;
     const auto ti = std::chrono::steady_clock::now();
-    HIPCHK(c, hipMemGetInfo(&freeb, &totb));
     const uint64_t need = seq_b + ws_b + out_b + msa_b + bp_w * 4 + uint64_t(nseg) * 8 + nz * (sizeof(ccsx::ZmwDesc) + 32);
-    if (need + (1ull << 30) > freeb + s.d_ws.cap + s.d_seq.cap + s.d_out.cap + s.d_msa.cap) {
-        char m[160];
-        snprintf(m, sizeof m, "batch needs %.1f GB of device memory, %.1f GB free: use a smaller chunk",
-                 need / 1e9, freeb / 1e9);
-        c->err = m;
-        return -1;
+    {
+        // a neighbour still holding memory: wait for it (ccsx_gpu_run has
+        // already cut the slice to what is free; a submitted batch cannot be cut)
+        bool fits = false;
+        const int r = wait_slot_mem(c, s, need, fits);
+        if (r) return r;
+        if (!fits) {
+            size_t freeb = 0, totb = 0;
+            HIPCHK(c, hipMemGetInfo(&freeb, &totb));
+            char m[200];
+            snprintf(m, sizeof m, "batch needs %.1f GB of device memory, %.1f GB free after waiting %u ms: use a smaller chunk",
+                     need / 1e9, freeb / 1e9, c->mem_wait_ms);
+            c->err = m;
+            return -1;
+        }
     }
     const bool timing = getenv("CCSX_TIMING") && atoi(getenv("CCSX_TIMING"));
     using tms = std::chrono::duration<double, std::milli>;
@@ -957,18 +1007,47 @@ int ccsx_gpu_run(ccsx_ctx *c, int mode, const ccsx_zmw_in *z, size_t nz, ccsx_zm
         while (b < idx.size()) {
             while (ci < cuts.size() && cuts[ci] <= b) ++ci;
             const size_t cut = ci < cuts.size() ? cuts[ci] : SIZE_MAX;
+            int si = next_slot;
+            next_slot ^= 1;
+            int r = collect(si);  // the slot's previous slice
+            if (r) return r;
+            // the slice as planned, cut further to what the device holds free
+            // for this slot now (a neighbour may still hold part of this
+            // context's share).  If not even its first ZMW fits, the other
+            // slot's arenas may hold the room: finish that slot's slice and
+            // stage there (the slices then run one after the other); else
+            // wait for a neighbour to release memory.
+            uint64_t lim = slot_budget;
+            {
+                uint64_t avail = 0;
+                if ((r = slot_avail(c, c->slot[si], avail))) return r;
+                const uint64_t x0 = zmw_bytes(z[idx[b]], full, c, c->shred_caps ? c->shred_read_cap : 0u);
+                if (avail < x0) {
+                    const int so = si ^ 1;
+                    if ((r = collect(so))) return r;
+                    uint64_t a2 = 0;
+                    if ((r = slot_avail(c, c->slot[so], a2))) return r;
+                    if (a2 > avail) si = so, avail = a2;  // (next_slot is already so: the next slice waits for this one)
+                }
+                if (avail < x0) {
+                    bool fits = false;
+                    if ((r = wait_slot_mem(c, c->slot[si], x0, fits))) return r;
+                    if ((r = slot_avail(c, c->slot[si], avail))) return r;
+                }
+                lim = std::min(lim, avail);
+            }
             uint64_t need = 0;
             size_t e = b;
             while (e < idx.size()) {
                 const uint64_t x = zmw_bytes(z[idx[e]], full, c, c->shred_caps ? c->shred_read_cap : 0u);
-                if (e > b && (need + x > slot_budget || cls[idx[e]] != cls[idx[b]] || e == cut)) break;
+                if (e > b && (need + x > lim || cls[idx[e]] != cls[idx[b]] || e == cut)) break;
                 need += x;
                 ++e;
             }
-            const int si = next_slot;
-            next_slot ^= 1;
-            int r = collect(si);  // the slot's previous slice
-            if (r) return r;
+            if (lim < slot_budget && (e < idx.size() && e != cut && need + zmw_bytes(z[idx[e]], full, c,
+                                                                                c->shred_caps ? c->shred_read_cap : 0u) <= slot_budget &&
+                                      cls[idx[e]] == cls[idx[b]]))
+                ++c->mem_replans;  // cut below the plan by the free memory
             sub.resize(e - b);
             for (size_t i = b; i < e; ++i) sub[i - b] = z[idx[i]];
             pend[si].idx = &idx;
@@ -1242,8 +1321,15 @@ int64_t ccsx_gpu_rerun_count(const ccsx_ctx *c) { return c ? (int64_t)c->reruns 
 int ccsx_gpu_run_stats(const ccsx_ctx *c, uint64_t *st, uint32_t n)
 {
     if (!c || !st) return -1;
-    const uint64_t v[4] = {c->reruns, c->slices, c->dealt, c->parts};
-    for (uint32_t i = 0; i < n && i < 4; ++i) st[i] = v[i];
+    const uint64_t v[6] = {c->reruns, c->slices, c->dealt, c->parts, c->mem_waits, c->mem_replans};
+    for (uint32_t i = 0; i < n && i < 6; ++i) st[i] = v[i];
+    return 0;
+}
+
+int ccsx_gpu_set_mem_wait(ccsx_ctx *c, uint32_t ms)
+{
+    if (!c) return -1;
+    c->mem_wait_ms = ms;
     return 0;
 }
 
@@ -1320,6 +1406,15 @@ int ccsx_gpu_set_prealloc(ccsx_ctx *c, int on)
 int ccsx_gpu_set_profiling(ccsx_ctx *c, int on)
 {
     if (!c) return -1;
+    if (on) {
+        // the product objects compile the counters out (KArgs::prof would
+        // receive zeros): only the diagnostic library can profile
+        for (int k = 0; k < ccsx::kCfgCount; ++k)
+            if (!kcfg_info(k).profiling) {
+                c->err = "the loaded kernel objects carry no phase counters: load libccsx_amd_diag.so";
+                return -1;
+            }
+    }
     c->profiling = on != 0;
     return 0;
 }

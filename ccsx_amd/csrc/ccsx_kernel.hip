@@ -2988,6 +2988,7 @@ extern "C" void CCSX_INFO(ccsx::KCfgInfo *o)
     o->ring_back = (uint32_t)ccsx::kRing;
     o->waves_per_simd = CCSX_WAVES_PER_EU;
     o->max_read = sizeof(K::RingT) == 2 ? K::kRing16MaxRead : 0u;
+    o->profiling = K::kProfiling ? 1u : 0u;
 }
 
 extern "C" hipError_t CCSX_LAUNCH(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s)

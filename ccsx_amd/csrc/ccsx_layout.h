@@ -66,6 +66,7 @@ struct KCfgInfo {
     uint32_t ring_rows, ring_back;
     uint32_t waves_per_simd;   // the object's register budget (amdgpu_waves_per_eu)
     uint32_t max_read;         // longest pushed read the object takes on the LDS instance (0: any)
+    uint32_t profiling;        // 1: the object carries the per-ZMW phase counters (diagnostic builds)
 };
 
 // per-ZMW status codes (0 = ok); any non-zero status is fatal for the batch

@@ -423,6 +423,25 @@ std::unordered_set<std::string> exclude_holes(std::string &buf, const char *arg)
 
 }  // namespace
 
+// CCSX_CHUNK / CCSX_CHUNK0 (measurement overrides) over the default last
+// chunk size cm_def (0: not known yet -- the device count decides it): the
+// last and first chunk sizes, computed the same way before and after the
+// devices open, the first never above the last.  Unknown sizes
+// come back 0.
+static void env_chunk_sizes(size_t cm_def, size_t &cm, size_t &c0)
+{
+    size_t ecm = 0, ec0 = 0;
+    if (const char *e = getenv("CCSX_CHUNK")) ecm = std::max<size_t>(1024, strtoull(e, nullptr, 10));
+    if (const char *e = getenv("CCSX_CHUNK0")) ec0 = std::min<size_t>(131072, std::max<size_t>(1, strtoull(e, nullptr, 10)));
+    cm = ecm ? ecm : cm_def;
+    if (ec0) {
+        c0 = ecm ? std::min(ec0, ecm) : ec0;
+        if (cm) cm = std::max(cm, c0);
+    } else {
+        c0 = cm ? std::max<size_t>(1024, cm / 2) : 0;
+    }
+}
+
 int main(int argc, char **argv)
 {
     const auto tmain = std::chrono::steady_clock::now();
@@ -699,10 +718,9 @@ int main(int argc, char **argv)
         // the sizes the environment fixes hold from the first record on (the
         // defaults depend on the device count, known once the devices open)
         size_t cm = 0, c0 = 0;
-        if (const char *e = getenv("CCSX_CHUNK")) cm = std::max<size_t>(1024, strtoull(e, nullptr, 10));
-        if (const char *e = getenv("CCSX_CHUNK0")) c0 = std::max<size_t>(1, strtoull(e, nullptr, 10));
-        if (cm) chunk_last = cm, chunk_first = c0 ? std::min(c0, cm) : std::max<size_t>(1024, cm / 2);
-        else if (c0) chunk_first = c0;
+        env_chunk_sizes(0, cm, c0);
+        if (cm) chunk_last = cm;
+        if (c0) chunk_first = c0;
     }
     ReadQueue rq(1);
     std::thread reader([&]() {
@@ -772,12 +790,10 @@ int main(int argc, char **argv)
         // the latency / occupancy objects while the device idled: 62,500
         // config-E ZMWs 6.3 s with 1,024, 5.4 s with 8,192, 5.8 s with 16,384,
         // r04e); CCSX_CHUNK / CCSX_CHUNK0 override
-        size_t cmax = std::min<size_t>((async ? 16384u : 8192u) * (size_t)n, 131072u);
-        if (const char *e = getenv("CCSX_CHUNK")) cmax = std::max<size_t>(1024, strtoull(e, nullptr, 10));
-        size_t c0 = std::max<size_t>(1024, cmax / 2);
-        if (const char *e = getenv("CCSX_CHUNK0")) c0 = std::max<size_t>(1, std::min<size_t>(cmax, strtoull(e, nullptr, 10)));
+        size_t cmax = 0, c0 = 0;
+        env_chunk_sizes(std::min<size_t>((async ? 16384u : 8192u) * (size_t)n, 131072u), cmax, c0);
         chunk_last = cmax;
-        chunk_first = c0;
+        chunk_first = c0;  // (the same first size the reader may already be filling to)
         ctx.assign(n, nullptr);
         std::vector<int> per_dev(ndev, 0);
         for (int i = 0; i < n; ++i) per_dev[(i / nslot) % ndev]++;

@@ -28,7 +28,7 @@ EXPORTS = {
                    "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count",
                    "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for",
                    "ccsx_gpu_run_stats", "ccsx_gpu_zmw_bytes", "ccsx_gpu_set_slot_budget", "ccsx_gpu_set_wg_cap",
-                   "ccsx_gpu_set_shred_read_cap", "ccsx_gpu_set_mem_frac",
+                   "ccsx_gpu_set_shred_read_cap", "ccsx_gpu_set_mem_frac", "ccsx_gpu_set_mem_wait",
                    "ccsx_gpu_slot_bytes", "ccsx_gpu_submit", "ccsx_gpu_collect", "ccsx_gpu_reserve_staging"],
     "ccsx_bspoa.h": ["init_bspoa", "beg_bspoa", "push_bspoa", "end_bspoa", "tidy_msa_bspoa", "free_bspoa"],
     "ccsx_host.h": ["ccsx_revcomp", "ccsx_prepare", "ccsx_prepare_apply", "ccsx_pairwise", "ccsx_synth_zmw",
@@ -93,6 +93,7 @@ def lib() -> C.CDLL:
         L.ccsx_gpu_set_shred_read_cap.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_mem_share.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_mem_frac.argtypes = [C.c_void_p, C.c_float]
+        L.ccsx_gpu_set_mem_wait.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_slot_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.ccsx_gpu_submit.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwIn), C.c_size_t, C.POINTER(C.c_int)]
         L.ccsx_gpu_collect.argtypes = [C.c_void_p, C.c_int, C.POINTER(ZmwOut)]
@@ -400,11 +401,17 @@ class Engine:
         return int(self._L.ccsx_gpu_rerun_count(self._ctx))
 
     def run_stats(self) -> dict:
-        """ccsx_gpu_run counters so far: reruns, slices, dealt lists, their parts."""
-        st = (C.c_uint64 * 4)()
-        if self._L.ccsx_gpu_run_stats(self._ctx, st, 4) != 0:
+        """ccsx_gpu_run counters so far: reruns, slices, dealt lists, their
+        parts, slices that waited for device memory, slices cut below the plan."""
+        st = (C.c_uint64 * 6)()
+        if self._L.ccsx_gpu_run_stats(self._ctx, st, 6) != 0:
             self._err("ccsx_gpu_run_stats")
-        return dict(zip(("reruns", "slices", "dealt", "parts"), (int(x) for x in st)))
+        return dict(zip(("reruns", "slices", "dealt", "parts", "mem_waits", "mem_replans"), (int(x) for x in st)))
+
+    def set_mem_wait(self, ms: int) -> None:
+        """How long a slice waits for device memory a neighbour still holds."""
+        if self._L.ccsx_gpu_set_mem_wait(self._ctx, ms) != 0:
+            self._err("ccsx_gpu_set_mem_wait")
 
     def zmw_bytes(self, z: Prepared, mode: int = MODE_SHRED) -> int:
         """Device bytes one ZMW occupies in a ccsx_gpu_run slice of `mode`."""
@@ -493,7 +500,10 @@ class Engine:
                   "tb_isteps", "tb_iruns", "tb_dsteps", "tb_druns")
 
     def set_profiling(self, on: bool = True) -> None:
-        self._L.ccsx_gpu_set_profiling(self._ctx, 1 if on else 0)
+        """Per-phase counters on / off; raises with the product library (its
+        objects carry none: CCSX_LIB=libccsx_amd_diag.so)."""
+        if self._L.ccsx_gpu_set_profiling(self._ctx, 1 if on else 0) != 0:
+            self._err("ccsx_gpu_set_profiling")
 
     def profile(self) -> dict:
         """Per-phase shader-clock cycles summed over the last launch's ZMWs."""

@@ -128,7 +128,9 @@ uint64_t ccsx_gpu_staged_bytes(const ccsx_ctx *ctx);
 
 /* Diagnostics: per-phase shader-clock counters (s_memtime) summed over the
  * ZMWs of the last launch: total, read staging, DP, traceback, merge,
- * columns, breakpoint+emission, DP rows.  Off by default. */
+ * columns, breakpoint+emission, DP rows.  Off by default.  Only the
+ * diagnostic library (libccsx_amd_diag.so) carries the counters: with the
+ * product library, turning them on returns -1 (ccsx_gpu_error says why). */
 int ccsx_gpu_set_profiling(ccsx_ctx *ctx, int on);
 /* Test hook: tight row capacity override (0 = default 3 x longest segment +
  * 4096, the segment capped at the 4,096-base window read buffer in shredded
@@ -158,8 +160,14 @@ int64_t ccsx_gpu_rerun_count(const ccsx_ctx *ctx);
 /* Counters of this context's ccsx_gpu_run calls so far, the first n of:
  * [0] ZMWs re-run with full caps, [1] slices launched, [2] ZMW lists dealt
  * into interleaved parts (a list of one launch class that needs k > 1 slots),
- * [3] the parts of those lists. */
+ * [3] the parts of those lists, [4] slices that waited for device memory a
+ * neighbour still held, [5] slices cut below the plan to the free memory. */
 int ccsx_gpu_run_stats(const ccsx_ctx *ctx, uint64_t *stats, uint32_t n);
+/* How long a slice waits for device memory that another context or a just
+ * exited process still holds before the call fails (default 60,000 ms).
+ * ccsx_gpu_run first cuts its slices to the free memory, then waits only if
+ * not even one ZMW fits; a ccsx_gpu_submit batch waits for its whole size. */
+int ccsx_gpu_set_mem_wait(ccsx_ctx *ctx, uint32_t ms);
 /* Device bytes ZMW *z occupies in a ccsx_gpu_run slice of `mode` (tight
  * capacities: workspace, subreads, output slab, tables). */
 uint64_t ccsx_gpu_zmw_bytes(const ccsx_ctx *ctx, int mode, const ccsx_zmw_in *z);

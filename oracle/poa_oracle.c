@@ -166,6 +166,36 @@ static inline int32_t getD(const opoa_t *g, uint32_t p, int64_t j)
     return g->Ds[(size_t)p * g->W + t];
 }
 
+/* Debug statistics (not part of the restatement): DP rows by the class the
+ * one-wave kernel objects give them (ccsx_kernel.hip dpS_row / dpA_cold, ring
+ * of OPOA_KRING rows).  Summed over every DP since the last reset; a process-
+ * wide counter, read single-threaded by tools/row_kinds.py. */
+#define OPOA_KRING 8
+enum { RK_FAST0, RK_FAST1, RK_CHAIN, RK_NP1, RK_NP2, RK_GEN, RK_FAR, RK_SPILL, RK_N };
+static uint64_t row_kinds[RK_N];
+void opoa_row_kinds(uint64_t *out, int reset)
+{
+    memcpy(out, row_kinds, sizeof row_kinds);
+    if (reset) memset(row_kinds, 0, sizeof row_kinds);
+}
+
+static void count_row_kind(const graph_t *G, uint32_t r, int32_t off, int32_t poff, const uint8_t *spill)
+{
+    const uint32_t np = G->poff[r + 1] - G->poff[r];
+    const uint32_t *pl = G->pred + G->poff[r];
+    int far = np > 4;
+    for (uint32_t s = 0; s < np; ++s) far |= r - pl[s] > OPOA_KRING;
+    if (spill[r]) row_kinds[RK_SPILL]++;
+    const int chain = np == 1 && pl[0] + 1 == r;
+    const int32_t sh = off - poff;
+    if (far) row_kinds[RK_FAR]++;
+    else if (chain && !spill[r] && (sh == 0 || sh == 1)) row_kinds[sh ? RK_FAST1 : RK_FAST0]++;
+    else if (chain && sh >= 0 && sh <= 2) row_kinds[RK_CHAIN]++;
+    else if (np == 1) row_kinds[RK_NP1]++;
+    else if (np == 2) row_kinds[RK_NP2]++;
+    else row_kinds[RK_GEN]++;
+}
+
 /* SPEC.md §3: banded read-vs-graph DP, rows in graph row order. */
 static void dp_align(opoa_t *g, const uint8_t *q, uint32_t m, uint32_t *er_out, uint32_t *ej_out)
 {
@@ -188,6 +218,10 @@ static void dp_align(opoa_t *g, const uint8_t *q, uint32_t m, uint32_t *er_out, 
     const int32_t lim = m > (uint32_t)W ? (int32_t)(m - W) : 0;
     int32_t bestE = INT32_MIN;
     uint32_t er = 0, ej = 0;
+    uint8_t *spill = calloc(R + 1, 1);
+    for (uint32_t r = 0; r < R; ++r)
+        for (uint32_t e = G->poff[r]; e < G->poff[r + 1]; ++e)
+            if (r - G->pred[e] > OPOA_KRING) spill[G->pred[e]] = 1;
     for (uint32_t r = 0; r < R; ++r) {
         const uint32_t np = G->poff[r + 1] - G->poff[r];
         const uint32_t *pl = G->pred + G->poff[r];
@@ -203,6 +237,7 @@ static void dp_align(opoa_t *g, const uint8_t *q, uint32_t m, uint32_t *er_out, 
             if (off > lim) off = lim;
         }
         g->roff[r] = off;
+        count_row_kind(G, r, off, r ? g->roff[r - 1] : 0, spill);
         int32_t *H = g->Hs + (size_t)r * W, *D = g->Ds + (size_t)r * W;
         uint8_t *cd = g->code + (size_t)r * W;
         uint16_t *msr = g->ms + (size_t)r * W, *dsr = g->ds + (size_t)r * W;
@@ -266,6 +301,7 @@ static void dp_align(opoa_t *g, const uint8_t *q, uint32_t m, uint32_t *er_out, 
         g->rmax[r] = rm;
         g->rarg[r] = ra;
     }
+    free(spill);
     g->cells += (uint64_t)R * (m < (uint32_t)W ? m : (uint32_t)W);
     *er_out = er;
     *ej_out = ej;

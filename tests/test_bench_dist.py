@@ -167,3 +167,51 @@ def test_concat_parts_in_rank_order(tmp_path):
     bench.concat_parts(parts, dst)
     assert open(dst, "rb").read() == want
     assert not any(os.path.exists(p) for p in parts)
+
+
+def test_traffic_keyed_by_the_launched_workload(tmp_path):
+    """a line's HBM traffic comes from a profile of the
+    same workload (key and cells per launch), never another one's; the
+    algorithmic bytes (2 bits per cell written and read back) sit beside it."""
+    import json
+    assert bench.traffic_key("B") == "B"
+    assert bench.traffic_key("B", nzmw=200) == "B_n200"
+    assert bench.traffic_key(None, roofline_zmws=16384) == "E16384"
+    assert bench.traffic_key(None, roofline_zmws=1024) == "E1024"
+    p = tmp_path / "traffic.json"
+    p.write_text(json.dumps({
+        "E16384": {"bytes_per_launch": 1000.0, "cells_per_launch": 400, "source": "profiles/x_summary.md"},
+        "B": {"bytes_per_launch": 50.0, "source": "profiles/old_summary.md"}}))
+    assert bench.traffic_entry("E1024", 400, str(p)) is None  # no profile of a 1,024-ZMW launch
+    e = bench.traffic_entry("E16384", 400, str(p))
+    assert e["key"] == "E16384" and e["cells_match"] is True
+    assert e["algorithmic_bytes"] == 400 * 2 * 2 / 8
+    assert e["traffic_over_algorithmic"] == round(1000.0 / 200.0, 2)
+    assert bench.traffic_entry("E16384", 401, str(p)) is None  # same key, another workload
+    assert bench.traffic_entry("B", 40, str(p))["algorithmic_bytes"] == 20.0
+    assert bench.traffic_entry("B_n200", 40, str(p)) is None
+
+
+def test_cli_timeline_parses_the_timing_log(tmp_path):
+    log = tmp_path / "cli.log"
+    log.write_text("[ccsx] 2 device context(s) open at 212 ms (main at epoch 1.0 s, 0 ms before)\n"
+                   "[ccsx] chunk 0: 100 ZMWs read 0-20 ms, prepared until 30 ms, 2 batches\n"
+                   "[ccsx] chunk 0 batch of 60 ZMWs on context 0: 233-1233 ms\n"
+                   "[ccsx] chunk 0 batch of 40 ZMWs on context 1: 240-1000 ms\n"
+                   "[ccsx] output done at 1300 ms; device cells 5; exit at epoch 2.0 s\n")
+    t = bench.cli_timeline(str(log))
+    assert t["open_ms"] == 212 and t["first_batch_ms"] == 233 and t["last_batch_end_ms"] == 1233
+    assert t["output_done_ms"] == 1300 and t["batched_zmws"] == 100 and t["batch_rate_zmws_per_s"] == 100.0
+    assert bench.cli_timeline(str(tmp_path / "missing.log")) == {}
+
+
+def test_one_process_line_devices_and_multi_node_skip(tmp_path):
+    """a multi-node job skips the one-process line with a reason
+    (the ranks' inputs live on their own nodes); its device list is the
+    CLI's context groups modulo the visible devices."""
+    import types
+    assert bench.one_process_devices(8, 8) == list(range(8))
+    assert bench.one_process_devices(2, 1) == [0]
+    args = types.SimpleNamespace(e_zmws=1000)
+    res = bench.one_process_line(args, 16, [None] * 16, [], str(tmp_path), str(tmp_path), local_world=8, ndev=8)
+    assert "multi-node" in res["skipped"]

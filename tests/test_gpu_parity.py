@@ -471,3 +471,96 @@ def test_submit_collect_pipeline(engine):
         engine.set_slot_budget(0)
     # ccsx_gpu_run still works on the same context afterwards
     assert [g for g, _, _ in engine.run(zs1[:3], cx.MODE_SHRED)] == want1[:3]
+
+
+class _DeviceHold:
+    """Device memory held by this process through the HIP runtime the
+    library uses (a stand-in for a neighbouring context or a just-exited
+    process whose memory the driver has not cleared yet)."""
+
+    def __init__(self):
+        import ctypes as C
+        self.C = C
+        self.hip = C.CDLL("libamdhip64.so.7" if _has_lib("libamdhip64.so.7") else "libamdhip64.so")
+        self.hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        self.hip.hipFree.argtypes = [C.c_void_p]
+        self.hip.hipMemGetInfo.argtypes = [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        self.ptrs = []
+
+    def free_bytes(self) -> int:
+        f, t = self.C.c_size_t(0), self.C.c_size_t(0)
+        assert self.hip.hipMemGetInfo(self.C.byref(f), self.C.byref(t)) == 0
+        return int(f.value)
+
+    def hold(self, nbytes: int) -> None:
+        p = self.C.c_void_p()
+        assert self.hip.hipMalloc(self.C.byref(p), nbytes) == 0, "hipMalloc of the hold failed"
+        self.ptrs.append(p)
+
+    def release(self) -> None:
+        while self.ptrs:
+            self.hip.hipFree(self.ptrs.pop())
+
+
+def _has_lib(name: str) -> bool:
+    import ctypes
+    try:
+        ctypes.CDLL(name)
+        return True
+    except OSError:
+        return False
+
+
+def test_run_with_device_memory_held():
+    """ccsx_gpu_run planned its slices from its share of
+    the device but staged them against what was free at the time, so a
+    context whose neighbour still held memory failed the call ("batch needs
+    28.2 GB of device memory, 25.7 GB free").  Now (1) a slice is cut to the
+    memory free for its slot, and (2) if not even one ZMW fits, the call
+    waits for a neighbour to release memory.  Both with results byte-equal
+    to the oracle."""
+    import threading
+    import time
+    zs = _e_zmws(10_700_000, 48)
+    eng = cx.Engine(0)
+    h = _DeviceHold()
+    try:
+        tot = sum(eng.zmw_bytes(z) for z in zs)
+        x0 = max(eng.zmw_bytes(z) for z in zs)
+        # (1) the plan says one slice of all of them; the device has room for ~1/3
+        eng.set_slot_budget(tot)
+        eng.set_mem_wait(2000)
+        h.hold(h.free_bytes() - (tot // 3 + (1 << 30) + (64 << 20)))
+        st0 = eng.run_stats()
+        _check(eng, zs, cx.MODE_SHRED, threads=16)
+        st = eng.run_stats()
+        assert st["mem_replans"] - st0["mem_replans"] >= 1, st
+        assert st["slices"] - st0["slices"] >= 3, st
+        h.release()
+        # (2) not even the largest ZMW fits; a neighbour frees its memory 1 s later
+        eng.close()
+        eng = cx.Engine(0)
+        eng.set_mem_wait(30000)
+        h.hold(h.free_bytes() - ((1 << 30) + x0 // 2))
+        t = threading.Timer(1.0, h.release)
+        t.start()
+        t0 = time.perf_counter()
+        st0 = eng.run_stats()
+        _check(eng, zs[:12], cx.MODE_SHRED, threads=16)
+        st = eng.run_stats()
+        t.join()
+        assert st["mem_waits"] - st0["mem_waits"] >= 1, st
+        assert time.perf_counter() - t0 >= 0.9
+    finally:
+        h.release()
+        eng.close()
+
+
+def test_profiling_needs_the_diagnostic_library(engine):
+    """the product objects compile the phase counters out, so
+    turning them on fails loudly instead of reporting zeros."""
+    import os
+    if "diag" in os.environ.get("CCSX_LIB", ""):
+        pytest.skip("the diagnostic library carries the counters")
+    with pytest.raises(cx.GpuError, match="phase counters"):
+        engine.set_profiling(True)

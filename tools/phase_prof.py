@@ -1,4 +1,8 @@
-"""Per-phase cycle breakdown of the consensus kernel (s_memtime counters)."""
+"""Per-phase cycle breakdown of the consensus kernel (s_memtime counters).
+
+Needs the diagnostic library, whose objects carry the counters:
+CCSX_LIB=libccsx_amd_diag.so python tools/phase_prof.py ...  (with the product
+library ccsx_gpu_set_profiling fails and this tool stops with its message)."""
 import argparse, os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import ccsx_amd as cx

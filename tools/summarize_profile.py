@@ -88,11 +88,16 @@ for f in ("kt_kernel_stats.csv",):
 # the bench config profiled (traffic.json key): the second argument, else the
 # tag's suffix (r04ze_E16384 -> E16384); never a silent default
 cfg = sys.argv[2] if len(sys.argv) > 2 else tag.rsplit("_", 1)[-1]
-if cfg not in ("B", "C", "D", "E", "H", "HP", "E16384"):
+if cfg not in ("B", "C", "D", "E", "H", "HP") and not cfg.startswith("E") and "_n" not in cfg:
     raise SystemExit(f"traffic.json key: pass the config as the second argument (tag suffix {cfg!r} is not one)")
+# the workload the PMC passes launched, so bench.py attaches this entry only
+# to a line that launched the same cells (bench.traffic_entry)
+pmc_b = json.loads(open(pmc1).read().strip().splitlines()[-1]) if os.path.exists(pmc1) else bench
+cells = (pmc_b.get("roofline") or {}).get("cells_per_launch") or pmc_b.get("cells_per_step")
 tj = os.path.join(ROOT, "profiles", "traffic.json")
 t = json.load(open(tj)) if os.path.exists(tj) else {}
 t[cfg] = {"bytes_per_launch": fetch_b + write_b, "fetch_bytes": fetch_b, "write_bytes": write_b,
+          "cells_per_launch": cells, "workload": pmc_b["config"]["workload"],
           "source": f"profiles/{tag}_summary.md (FETCH_SIZE+WRITE_SIZE in KB x1024, raw; FETCH_SIZE "
                     f"would be x2 only for wide coalesced streams)"}
 json.dump(t, open(tj, "w"), indent=1)

@@ -1,5 +1,6 @@
 """Distribution of per-ZMW kernel cycles (development tool): the launch ends
-with its slowest ZMW, so the tail, not the mean, sets ms per step."""
+with its slowest ZMW, so the tail, not the mean, sets ms per step.
+Needs CCSX_LIB=libccsx_amd_diag.so (the product objects carry no counters)."""
 import argparse, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import ccsx_amd as cx
@@ -14,7 +15,7 @@ if a.nzmw:
     cfg["nzmw"] = a.nzmw
 zs = bench.make_batch(cfg, 0)
 e = cx.Engine(0)
-e.stage(zs, a.mode)
+e.stage(zs, cfg["mode"])
 plain = [e.launch(cfg["mode"]) for _ in range(3)]
 e.set_profiling(True)
 ms = e.launch(cfg["mode"])
