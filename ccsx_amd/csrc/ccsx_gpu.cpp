@@ -29,16 +29,18 @@ extern "C" hipError_t ccsx_launch_zmw_occ(const ccsx::KArgs *a, uint32_t lds_byt
 extern "C" hipError_t ccsx_launch_zmw_tput(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" hipError_t ccsx_launch_zmw_solo(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" hipError_t ccsx_launch_zmw_solo16(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
+extern "C" hipError_t ccsx_launch_zmw_solo16w(const ccsx::KArgs *a, uint32_t lds_bytes, hipStream_t s);
 extern "C" void ccsx_kcfg_info_lat(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_occ(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_tput(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_solo(ccsx::KCfgInfo *o);
 extern "C" void ccsx_kcfg_info_solo16(ccsx::KCfgInfo *o);
+extern "C" void ccsx_kcfg_info_solo16w(ccsx::KCfgInfo *o);
 
 namespace {
 typedef hipError_t (*LaunchFn)(const ccsx::KArgs *, uint32_t, hipStream_t);
-constexpr LaunchFn kLaunch[ccsx::kCfgCount] = {ccsx_launch_zmw_lat, ccsx_launch_zmw_occ, ccsx_launch_zmw_tput,
-                                               ccsx_launch_zmw_solo, ccsx_launch_zmw_solo16};
+constexpr LaunchFn kLaunch[ccsx::kCfgCount] = {ccsx_launch_zmw_lat,  ccsx_launch_zmw_occ,    ccsx_launch_zmw_tput,
+                                               ccsx_launch_zmw_solo, ccsx_launch_zmw_solo16, ccsx_launch_zmw_solo16w};
 
 ccsx::KCfgInfo kcfg_info(int cfg)
 {
@@ -47,7 +49,8 @@ ccsx::KCfgInfo kcfg_info(int cfg)
     else if (cfg == ccsx::kCfgOccupancy) ccsx_kcfg_info_occ(&o);
     else if (cfg == ccsx::kCfgThroughput) ccsx_kcfg_info_tput(&o);
     else if (cfg == ccsx::kCfgSolo) ccsx_kcfg_info_solo(&o);
-    else ccsx_kcfg_info_solo16(&o);
+    else if (cfg == ccsx::kCfgSolo16) ccsx_kcfg_info_solo16(&o);
+    else ccsx_kcfg_info_solo16w(&o);
     return o;
 }
 
@@ -365,6 +368,8 @@ constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
 // slices of at least this many times the occupancy configuration's resident
 // workgroups run the solo configuration
 constexpr size_t kSoloSliceFactor = 3;
+// segments per ZMW (slice mean) below which a solo16 slice runs solo16w
+constexpr uint32_t kSolo16WMaxSegs = 16;
 
 // launch classes of ccsx_gpu_run's slices: LDS read buffer up to 32 kb (4+
 // workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never
@@ -529,12 +534,20 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
         const size_t res_occ = (size_t)c->ncu * kcfg_wg_per_cu(ccsx::kCfgOccupancy, extra);
         s.cfg = nz <= res_lat ? ccsx::kCfgLatency : nz < kSoloSliceFactor * res_occ ? ccsx::kCfgOccupancy
                                                                                   : ccsx::kCfgSolo16;
+        // solo16 at 80 VGPRs, 24 workgroups per CU (solo16w), where the
+        // slice's ZMWs have few segments: their DPs' rows are mostly the fast
+        // chain rows, which stay in registers at 80 VGPRs (16,384 config-E
+        // ZMWs per launch: 582 -> 569 ms); many segments make the multi-
+        // predecessor rows, whose predecessor lists then live in scratch,
+        // frequent (config D, 30 passes: 314 -> 319 ms), so those keep 96
+        // VGPRs and 20 per CU (r06c)
+        if (s.cfg == ccsx::kCfgSolo16 && nseg < (uint64_t)kSolo16WMaxSegs * nz) s.cfg = ccsx::kCfgSolo16W;
         if (c->cfg_force >= 0) s.cfg = c->cfg_force;
         // solo16 (int16 ring) takes the LDS instance with pushed reads of at
         // most its max_read bases (a tight-cap shredded slice pushes at most
         // its read cap); other slices run the solo object, forced or not
-        if (s.cfg == ccsx::kCfgSolo16) {
-            const uint32_t mr = kcfg_info(ccsx::kCfgSolo16).max_read;
+        if (s.cfg == ccsx::kCfgSolo16 || s.cfg == ccsx::kCfgSolo16W) {
+            const uint32_t mr = kcfg_info(s.cfg).max_read;
             const uint32_t pushed = shred_tight ? std::min(lmax_all, c->shred_read_cap) : lmax_all;
             if (!s.lds_read_words || (mr && pushed > mr)) s.cfg = ccsx::kCfgSolo;
         }

@@ -129,6 +129,27 @@ __device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old
 
 __device__ __forceinline__ int wave_shl1(int old, int v) { return dpp<0x130>(old, v); }  // lane l <- l+1
 
+// K a + C and K a for |a| < 2^23 (v_mad_i32_i24 / v_mul_i32_i24, full rate;
+// the compiler cannot see the operand's range across the DP's basic blocks
+// and emits the quarter-rate v_mul_lo_u32).  K, C inline constants (-16..64)
+template <int K, int C>
+__device__ __forceinline__ int32_t mad24(int32_t a)
+{
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(K), "i"(C));
+    return r;
+}
+template <int K>
+__device__ __forceinline__ int32_t mul24(int32_t a)
+{
+    int32_t r;
+    asm("v_mul_i32_i24 %0, %2, %1" : "=v"(r) : "v"(a), "i"(K));
+    return r;
+}
+
+// lane l <- l-1, lane 0 <- 0 (the DPP bound control: no old-value register)
+__device__ __forceinline__ int wave_shr1_z(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
+
 // lane `l` of v <- the uniform value x (v_writelane_b32; l and x in SGPRs)
 __device__ __forceinline__ int writelane(int v, int x, int l)
 {
@@ -633,7 +654,8 @@ __device__ __forceinline__ void pred_terms_n(const RingT *ring, uint32_t r, int3
                                              int32_t o0, int32_t o1, int lane, PredAcc &A)
 {
     const int32_t s0 = off - o0, s1 = off - o1;
-    const bool inr = (uint32_t)(s0 + 3) <= 7u && (NP < 2 || (uint32_t)(s1 + 3) <= 7u);
+    // (one unsigned max: fewer scalar compares and selects than an &&)
+    const bool inr = (NP < 2 ? (uint32_t)(s0 + 3) : max((uint32_t)(s0 + 3), (uint32_t)(s1 + 3))) <= 7u;
     constexpr int dd = kDc - kHc + 1;
     if (__builtin_expect(inr, 1)) {
         const int L2 = 2 * lane;
@@ -759,7 +781,17 @@ struct AState {
 // per-lane constants of a row (t0 = 2 lane, t1 = t0 + 1)
 struct LaneK {
     int32_t L2, L4, kc0, kc1, cI0, cI1, src0;  // src0: O + E t0
+    // the one-wave DP's tail (dpS_row): X = H' - E t biased by kXBias, so every
+    // real X is positive and the scans' out-of-range lanes can read 0 from the
+    // DPP bound control (no old-value register per shift, no copy of the
+    // scan's input); the insertion term of cell 1 carries -kXBias (cell 0's is
+    // cIb1 + 2: at lane 0, where the exclusive prefix max is 0, that is
+    // -kXBias - 3, below every real H', i.e. I(0) = NEG)
+    int32_t cIb1;
 };
+// 2^30: the bit pattern of 2.0f, an inline constant (v_add3_u32 takes it
+// without a register); every |X| of a read < 2^22 is below 2^24
+constexpr int32_t kXBias = 1 << 30;
 
 __device__ __forceinline__ LaneK lane_consts(int lane)
 {
@@ -768,6 +800,7 @@ __device__ __forceinline__ LaneK lane_consts(int lane)
     c.kc0 = 127 - c.L2, c.kc1 = 126 - c.L2;
     c.cI0 = kO + kE * c.L2, c.cI1 = kO + kE * (c.L2 + 1);
     c.src0 = kO + kE * c.L2;
+    c.cIb1 = c.cI1 - kXBias;
     return c;
 }
 
@@ -1149,6 +1182,62 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
     __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, (((uint32_t)lane * 4u + x.rot) & 255u) + x.ioff, x.sbase, 0);
 }
 
+// row_record for the one-wave DP (dpS_row): the same records and free-end
+// candidates from its biased X (LaneK::xb*: X + kXBias, the exclusive prefix
+// max 0 at lane 0), and, on FULL rows, the lane's candidate from xm = max(X0,
+// X1), the insertion scan's input: one add, a compare for the cell and a
+// carry-in add for the key (round 5: two adds, a max, two compares, a select
+// and a shift-or per row)
+template <bool FULL>
+__device__ __forceinline__ void row_record_solo(Z &z, int32_t &bE, uint32_t &bKey, const __amdgpu_buffer_rsrc_t &rc,
+                                                uint32_t r, uint32_t m, int32_t lim, int32_t off, uint32_t np,
+                                                bool maybe_wide, const PredAcc &A, const LaneK &c, bool mp0, bool mp1,
+                                                bool d0, bool d1, int32_t hp0, int32_t hp1, int32_t X0, int32_t X1,
+                                                int32_t xm, int32_t Pex, int32_t ex1, const RowX &x)
+{
+    const int lane = lane_id();
+    const int32_t X1L = wave_shr1_z(X1);  // lane 0: 0 (t = 0 has no extension)
+    const bool i0 = Pex + c.cIb1 + 2 > hp0, i1 = ex1 + c.cIb1 > hp1;
+    const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
+    const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
+    const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
+    uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
+    uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
+    if (maybe_wide && __builtin_expect(np > 63u, 0)) {
+        reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
+            make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
+    }
+    // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1 = X + eb
+    // (x.em1 carries -kXBias), and H' at j = m - 1 (+3)
+    const int32_t eb = (off << 1) + x.em1;
+    if (FULL) {
+        int32_t e01;
+        uint32_t c1;
+        if (__builtin_expect(off == lim, 0)) {
+            // the band meets the read's end: cell 127 is j = m - 1
+            const int32_t X1e = writelane(X1, __builtin_amdgcn_readlane(X1, 63) + 3, 63);
+            c1 = X1e > X0 ? 1u : 0u;
+            e01 = max(X0, X1e) + eb;
+        } else {
+            c1 = X1 > X0 ? 1u : 0u;
+            e01 = xm + eb;
+        }
+        // the lane's cell 1 only if strictly better, then against the best
+        // so far (rows come in order: the first maximum is the earliest)
+        if (e01 > bE) bE = e01, bKey = r * 2 + c1;
+    } else {
+        int32_t e0 = X0 + eb, e1 = X1 + eb;
+        if ((uint32_t)c.L2 == m - 1) e0 += 3;
+        if ((uint32_t)c.L2 + 1 == m - 1) e1 += 3;
+        if ((uint32_t)c.L2 >= m) e0 = INT32_MIN, w0 = 0;
+        if ((uint32_t)c.L2 + 1 >= m) e1 = INT32_MIN, w1 = 0;
+        const bool c1 = e1 > e0;
+        const int32_t e01 = c1 ? e1 : e0;
+        if (e01 > bE) bE = e01, bKey = r * 2 + (c1 ? 1u : 0u);
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, (((uint32_t)lane * 4u + x.rot) & 255u) + x.ioff, x.sbase, 0);
+}
+
 // helper wave: everything after the predecessor terms of row r (SPEC.md
 // §3.2-§3.5): M, H', the insertion scan, the cell codes and tags, the
 // free-end candidates, the record store
@@ -1402,29 +1491,43 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
     auto tail = [&](int32_t off, uint32_t qp, const PredAcc &A, bool cold) __attribute__((always_inline)) {
         // the next row's read window, a row ahead of its use
         S.qn = rd_win16(z, off, z.hbm && win_has(z.wa, 2, off));
-        // the source terms O + E j (0 at j = 0) from VALU arithmetic alone
-        // (a select on off == 0 && lane == 0 cost four SALU per row)
-        const int32_t j0 = off + c.L2;
-        const int32_t srcu = kO + kE * j0;
-        const int32_t src0 = srcu - kO * (1 - min(j0, 1));
-        const bool mp0 = A.Mh0 >= src0, mp1 = A.Mh1 >= srcu + kE;
-        const int32_t M0 = max(A.Mh0, src0) + ((qp & 3u) == base ? kMs : kXs);
-        const int32_t M1 = max(A.Mh1, srcu + kE) + (((qp >> 2) & 3u) == base ? kMs : kXs);
+        const int32_t j0 = off + c.L2;  // < 2^22 + 128 (dp_align): 24-bit multiplies
+        // the source terms (SPEC.md §3.2) O + E j, 0 at j = 0: cell 0's is
+        // max((O + E) j, O + E j) for every j >= 0 (O < 0), folded into M's
+        // max as one max3 (mp: the predecessor term is that max); cell 1's j
+        // is never 0 (round 5: a min / select chain of 7 VALU per row)
+        const int32_t src1 = mad24<kE, kO + kE>(j0);
+        const int32_t Mx0 = max(max(A.Mh0, mul24<kO + kE>(j0)), mad24<kE, kO>(j0));
+        const bool mp0 = Mx0 == A.Mh0, mp1 = A.Mh1 >= src1;
+        const int32_t M0 = Mx0 + ((qp & 3u) == base ? kMs : kXs);
+        const int32_t M1 = max(A.Mh1, src1) + (((qp >> 2) & 3u) == base ? kMs : kXs);
         int32_t Dv0 = A.Dv0, Dv1 = A.Dv1;
         const bool d0 = Dv0 > M0, d1 = Dv1 > M1;
         const int32_t hp0 = max(M0, Dv0), hp1 = max(M1, Dv1);
-        const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
-        int32_t incl = max(X0, X1);
+        // X biased by kXBias (LaneK): positive for every real H'
+        const int32_t X0 = hp0 + c.L4 + kXBias, X1 = hp1 + (c.L4 + 2) + kXBias;
+        const int32_t xm = max(X0, X1);  // the lane's larger X: the scan's input, its free-end candidate
         int32_t rk0 = (hp0 << 7) | c.kc0, rk1 = (hp1 << 7) | c.kc1;
         if (!FULL) {
             if ((uint32_t)c.L2 >= m) rk0 = INT32_MIN, Dv0 = kNeg;
             if ((uint32_t)c.L2 + 1 >= m) rk1 = INT32_MIN, Dv1 = kNeg;
         }
         int32_t rk = max(rk0, rk1);
-        wave_incl_max2(incl, rk);
-        const int32_t Pex = wave_shr1(kNeg, incl);
+        // the insertion scan's first step reads 0 (the bound control) where
+        // row_shr has no source: max(0, X) = X, and its result goes to a new
+        // register (xm stays); the row-key scan as before
+        int32_t incl = max(xm, __builtin_amdgcn_update_dpp(0, xm, 0x111, 0xF, 0xF, true));
+        incl = dpp_max<0x112>(incl);
+        incl = dpp_max<0x114>(incl);
+        incl = dpp_max<0x118>(incl);
+        incl = dpp_max<0x142, 0xA>(incl);
+        incl = dpp_max<0x143, 0xC>(incl);
+        rk = wave_incl_max(rk);
+        // exclusive prefix max; lane 0 gets 0, below every biased X: its cell
+        // 0 insertion term Pex + cIb1 + 2 is -kXBias - 3, i.e. I(0) = NEG
+        const int32_t Pex = wave_shr1_z(incl);
         const int32_t ex1 = max(Pex, X0);
-        int32_t nH0 = max(Pex + c.cI0, hp0), nH1 = max(ex1 + c.cI1, hp1);
+        int32_t nH0 = max(Pex + c.cIb1 + 2, hp0), nH1 = max(ex1 + c.cIb1, hp1);
         if (!FULL) {
             if ((uint32_t)c.L2 >= m) nH0 = kNegH;
             if ((uint32_t)c.L2 + 1 >= m) nH1 = kNegH;
@@ -1451,9 +1554,8 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         S.pArg = off + kW / 2 - (key & 127);
         // decision bits, free-end candidates, record (only a cold row can
         // have more than 63 predecessors)
-        int32_t no_off = 0;
-        row_record<FULL, false>(z, B.bE, B.bKey, no_off, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0,
-                         X1, Pex, x);
+        row_record_solo<FULL>(z, B.bE, B.bKey, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0, X1,
+                              xm, Pex, ex1, x);
     };
     if (__builtin_expect(fast, 1)) {
         // the only predecessor is row r - 1 (tag 1), band moved by 0 or 1:
@@ -1531,7 +1633,7 @@ __device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0,
     static_assert(kBlkAB <= 16 && 32 % kBlkAB == 0, "a block's rows share tb_rot's 32-row period");
     const uint32_t fm = (uint32_t)(S.fmask >> (r0 & 63u));
     const uint32_t rot0 = tb_rot(r0);
-    const int32_t em1 = -2 * (int32_t)m - 1;
+    const int32_t em1 = -2 * (int32_t)m - 1 - kXBias;  // (row_record_solo: X is biased)
     if (r0 + kBlkAB <= R) {
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i)

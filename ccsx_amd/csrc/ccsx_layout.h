@@ -59,7 +59,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 // Each configuration's object reports its own LDS words and threads
 // (KCfgInfo), so the host never restates the build flags.
 enum KernelCfg : int32_t { kCfgLatency = 0, kCfgOccupancy = 1, kCfgThroughput = 2, kCfgSolo = 3, kCfgSolo16 = 4,
-                           kCfgCount = 5 };
+                           kCfgSolo16W = 5, kCfgCount = 6 };
 struct KCfgInfo {
     uint32_t lds_fixed_words;  // LDS words before the read buffer
     uint32_t threads;          // workgroup size

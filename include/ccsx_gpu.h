@@ -146,12 +146,14 @@ int ccsx_gpu_set_tight_out(ccsx_ctx *ctx, uint32_t bytes);
 int ccsx_gpu_set_stage_piece(ccsx_ctx *ctx, uint64_t bytes);
 /* Kernel configuration of the next slices: -1 (default) = by slice size (the
  * latency configuration 0 -- three waves, 8-row DP blocks, 32-row LDS ring --
- * when it keeps the whole slice resident; the solo configuration 3 -- one
- * wave per ZMW, 8-row ring, 14-16 ZMWs per CU -- for slices of at least 3x
- * what the occupancy one keeps resident; else the occupancy configuration 1
- * -- 4-row blocks, 24-row ring, one more workgroup per CU); 0 / 1 / 2 / 3
+ * when it keeps the whole slice resident; for slices of at least 3x what the
+ * occupancy one keeps resident a one-wave-per-ZMW configuration with an int16
+ * ring: 5 (solo16w, 24 per CU) when the slice's ZMWs average fewer than 16
+ * segments, else 4 (solo16, 20 per CU), or 3 (solo, int32 ring) where a
+ * pushed read exceeds 16,256 bases or the slice runs the HBM-read instance;
+ * else the occupancy configuration 1 -- 4-row blocks, 24-row ring); 0 .. 5
  * force one (2: the throughput configuration, two-wave workgroups, up to 8
- * per CU, only by this call).
+ * per CU, only by this call; a forced 4 / 5 the int16 ring cannot take runs 3).
  * ccsx_gpu_kernel_cfg: the configuration of the last staged slice. */
 int ccsx_gpu_set_kernel_cfg(ccsx_ctx *ctx, int cfg);
 int ccsx_gpu_kernel_cfg(const ccsx_ctx *ctx);

@@ -101,7 +101,7 @@ def test_bench_two_ranks_on_device():
     assert two["cli"]["sample_equal"] == two["cli"]["sample"] == 12
     assert two["value"] > 0 and two["e2e"]["value"] > 0
     assert two["e2e"]["sample_equal"] == two["e2e"]["sample"] == 64
-    assert one["roofline"]["kernel_cfg"] in (0, 1, 3, 4) and one["scaling"] == "strong"
+    assert one["roofline"]["kernel_cfg"] in (0, 1, 3, 4, 5) and one["scaling"] == "strong"
     # the job's CPU share split over the two local ranks, each bound
     share = bench.cpu_share()[0]
     assert one["config"]["cli_jobs"] == share and one["config"]["cli_cpus"] == "unbound"

@@ -32,6 +32,10 @@ def main() -> None:
     ap.add_argument("--hole0", type=int, default=bench.E_HOLE0)
     ap.add_argument("--jobs", default="2,4,8,16")
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--settle", type=float, default=15.0,
+                    help="idle seconds before each run: the driver clears the device memory a process freed "
+                         "lazily, and the next process's first large allocation waits for it (DESIGN.md §7) -- "
+                         "free memory alone (tools/mem_wait.py) does not show it")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -48,6 +52,7 @@ def main() -> None:
     try:
         for rep in range(a.repeat):
             for j in [int(x) for x in a.jobs.split(",")]:
+                time.sleep(a.settle)
                 mw = bench.wait_device_memory([0])
                 cpus = allowed[:j]
                 os.sched_setaffinity(0, cpus)
@@ -58,7 +63,7 @@ def main() -> None:
                 finally:
                     os.sched_setaffinity(0, allowed)
                 tl = bench.cli_timeline(log)
-                r = {"jobs": j, "cpus": bench.cpu_ranges(cpus), "rep": rep, "mem_wait_s": mw["mem_wait_s"],
+                r = {"jobs": j, "cpus": bench.cpu_ranges(cpus), "rep": rep, "settle_s": a.settle, "mem_wait_s": mw["mem_wait_s"],
                      "cli_s": round(dt, 3), "zmws_per_s": round(a.n / dt, 1), "records": scan["nrec"],
                      "in_order": scan["in_order"], "timeline": tl}
                 if "first_batch_ms" in tl:
