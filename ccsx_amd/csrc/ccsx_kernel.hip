@@ -437,22 +437,43 @@ __device__ __forceinline__ uint32_t win_codes(uint32_t win, int32_t off, int32_t
     return win >> ((((uint32_t)off + 2u * lane_id()) & 3u) * 2u + 2u * (uint32_t)d);
 }
 
-// per lane: row r0+lane's info and first four predecessors
+// per lane: row r0+lane's info and first four predecessors (the one-wave
+// objects: the four predecessors' row distances, 8 bits each, in dpk -- a
+// row without the far flag has every predecessor within kRing rows -- two
+// VGPRs per 64-row window instead of five)
 struct RowPre {
-    uint32_t info, po, p0, p1, p2, p3;
+    uint32_t info, po, p0, p1, p2, p3, dpk;
 };
 // row info bits: base (0-1) | spill (2: a successor lies > kRing rows ahead)
 // | chain (3: the only predecessor is the previous row) | far (4: a
 // predecessor lies > kRing rows back or there are > 4) | np << 8
 constexpr uint32_t kInfoSpill = 4u, kInfoChain = 8u, kInfoFar = 16u;
 
+// predecessor k (< 4) of row r = r0 + li of a non-far row, from the window
+__device__ __forceinline__ uint32_t row_pred(const RowPre &W, uint32_t r, int li, int k)
+{
+    if constexpr (kHelpers == 0) {
+        const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)W.dpk, li);
+        return r - ((dk >> (8 * k)) & 255u);
+    }
+    const uint32_t v = k == 0 ? W.p0 : k == 1 ? W.p1 : k == 2 ? W.p2 : W.p3;
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, li);
+}
+
 // the DP's row records (written by merge): coalesced, no dependent loads
 __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o)
 {
     const uint32_t n = r0 < z.R ? z.R - r0 : 0u;
+    const uint32_t sp = __builtin_amdgcn_raw_buffer_load_b8(brsrc(P<const uint8_t>(z, z.L.spf) + r0, n), lane_id(), 0, 0);
+    if constexpr (kHelpers == 0) {
+        // {info, dpk} (merge writes them so on the one-wave objects)
+        const v2u q = __builtin_amdgcn_raw_buffer_load_b64(brsrc(P<const uint4>(z, z.L.rrec) + r0, n * 16),
+                                                           lane_id() * 16, 0, 0);
+        o.info = q.x | (sp ? kInfoSpill : 0u), o.dpk = q.y;
+        return;
+    }
     const v4u q = __builtin_amdgcn_raw_buffer_load_b128(brsrc(P<const uint4>(z, z.L.rrec) + r0, n * 16),
                                                         lane_id() * 16, 0, 0);
-    const uint32_t sp = __builtin_amdgcn_raw_buffer_load_b8(brsrc(P<const uint8_t>(z, z.L.spf) + r0, n), lane_id(), 0, 0);
     o.info = q.x | (sp ? kInfoSpill : 0u), o.p0 = q.y, o.p1 = q.z, o.p2 = q.w;
     o.p3 = __builtin_amdgcn_raw_buffer_load_b32(brsrc(P<const uint32_t>(z, z.L.rp3) + r0, n * 4), lane_id() * 4, 0, 0);
 }
@@ -838,15 +859,15 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
         pred_fold<SLOTS>(A, 0, 1u, hA, hB, hC, dB, dC);  // the predecessor is row r - 1
     } else if (np == 1) {
         kind = 2;
-        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
+        const uint32_t p0 = row_pred(S.W.cur, r, li, 0);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
         const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
         off = min(max(o0 + 127 - (k0 & 127) + 1 - kW / 2, 0), lim);
         pred_terms_n<1, SLOTS>(ring, r, off, p0, p0, o0, o0, lane, A);
     } else if (np == 2) {
         kind = 3;
-        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
-        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
+        const uint32_t p0 = row_pred(S.W.cur, r, li, 0);
+        const uint32_t p1 = row_pred(S.W.cur, r, li, 1);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
         const int32_t o1 = __builtin_amdgcn_readlane(S.vOff, (int)(p1 & 63u));
         const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
@@ -857,10 +878,10 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
         off = min(max(oo + 127 - (ko & 127) + 1 - kW / 2, 0), lim);
         pred_terms_n<2, SLOTS>(ring, r, off, p0, p1, o0, o1, lane, A);
     } else {
-        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
-        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
-        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p2, li);
-        const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p3, li);
+        const uint32_t p0 = row_pred(S.W.cur, r, li, 0);
+        const uint32_t p1 = row_pred(S.W.cur, r, li, 1);
+        const uint32_t p2 = row_pred(S.W.cur, r, li, 2);
+        const uint32_t p3 = row_pred(S.W.cur, r, li, 3);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
         const int32_t o1 = __builtin_amdgcn_readlane(S.vOff, (int)(p1 & 63u));
         const int32_t o2 = __builtin_amdgcn_readlane(S.vOff, (int)(p2 & 63u));
@@ -2642,8 +2663,17 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
             if (n - ad > (uint32_t)kRing) spf[ad] = 1, far = kInfoFar;
         }
         const uint32_t chain = (np == 1 && ps[0] + 1 == n) ? kInfoChain : 0u;
-        rrec[n] = make_uint4((nb[x] & 3u) | chain | far | (np << 8), ps[0], ps[1], ps[2]);
-        rp3[n] = ps[3];
+        const uint32_t info = (nb[x] & 3u) | chain | far | (np << 8);
+        if constexpr (kHelpers == 0) {
+            // {info, the predecessors' row distances} (RowPre::dpk; only read on rows without the far flag)
+            uint32_t dpk = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) dpk |= ((uint32_t)u < np ? (n - ps[u]) & 255u : 0u) << (8 * u);
+            *reinterpret_cast<uint2 *>(rrec + n) = make_uint2(info, dpk);
+        } else {
+            rrec[n] = make_uint4(info, ps[0], ps[1], ps[2]);
+            rp3[n] = ps[3];
+        }
       }
     }
     for (uint32_t i = tid; i < K; i += T) {
@@ -2655,8 +2685,12 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
             if (n - ad > (uint32_t)kRing) spf[ad] = 1;
             info |= (1u << 8) | (ad + 1 == n ? kInfoChain : 0u) | (n - ad > (uint32_t)kRing ? kInfoFar : 0u);
         }
-        rrec[n] = make_uint4(info, ad != kNone ? ad : 0u, 0u, 0u);
-        rp3[n] = 0;
+        if constexpr (kHelpers == 0) {
+            *reinterpret_cast<uint2 *>(rrec + n) = make_uint2(info, ad != kNone ? (n - ad) & 255u : 0u);
+        } else {
+            rrec[n] = make_uint4(info, ad != kNone ? ad : 0u, 0u, 0u);
+            rp3[n] = 0;
+        }
     }
         DP_STAMP(kPfRowE);
     // M5: first/last rows of the reads
