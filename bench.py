@@ -694,13 +694,12 @@ def traffic_entry(key: str, cells_per_launch: int, path: str | None = None):
     the traceback (north_star's 2-bit traceback matrices), so the ratio says
     how far the HBM traffic is above that."""
     t = load_traffic(key, path)
-    if t is None:
-        return None
+    if t is None or t.get("cells_per_launch") is None:
+        return None  # no profile of this workload (or one too old to say which cells it launched)
     out = dict(t, key=key)
-    if t.get("cells_per_launch") is not None:
-        out["cells_match"] = int(t["cells_per_launch"]) == int(cells_per_launch)
-        if not out["cells_match"]:
-            return None  # the profile measured a different workload under this key
+    out["cells_match"] = int(t["cells_per_launch"]) == int(cells_per_launch)
+    if not out["cells_match"]:
+        return None  # the profile measured a different workload under this key
     alg = cells_per_launch * 2 * 2 / 8
     out["algorithmic_bytes"] = alg
     if alg and t.get("bytes_per_launch"):

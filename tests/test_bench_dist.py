@@ -181,7 +181,8 @@ def test_traffic_keyed_by_the_launched_workload(tmp_path):
     p = tmp_path / "traffic.json"
     p.write_text(json.dumps({
         "E16384": {"bytes_per_launch": 1000.0, "cells_per_launch": 400, "source": "profiles/x_summary.md"},
-        "B": {"bytes_per_launch": 50.0, "source": "profiles/old_summary.md"}}))
+        "B": {"bytes_per_launch": 50.0, "cells_per_launch": 40, "source": "profiles/b_summary.md"},
+        "D": {"bytes_per_launch": 70.0, "source": "profiles/old_summary.md"}}))
     assert bench.traffic_entry("E1024", 400, str(p)) is None  # no profile of a 1,024-ZMW launch
     e = bench.traffic_entry("E16384", 400, str(p))
     assert e["key"] == "E16384" and e["cells_match"] is True
@@ -190,6 +191,7 @@ def test_traffic_keyed_by_the_launched_workload(tmp_path):
     assert bench.traffic_entry("E16384", 401, str(p)) is None  # same key, another workload
     assert bench.traffic_entry("B", 40, str(p))["algorithmic_bytes"] == 20.0
     assert bench.traffic_entry("B_n200", 40, str(p)) is None
+    assert bench.traffic_entry("D", 40, str(p)) is None  # an old profile that did not record its cells
 
 
 def test_cli_timeline_parses_the_timing_log(tmp_path):
