@@ -547,6 +547,10 @@ int main(int argc, char **argv)
     // a context with no more work releases its memory while the others run
     // (CCSX_EARLY_CLOSE=0: the exit releases everything)
     const bool early_close = !(getenv("CCSX_EARLY_CLOSE") && atoi(getenv("CCSX_EARLY_CLOSE")) == 0);
+    // the last context too, while the writer emits the last chunks: the exit
+    // then has less to release (62,500 config-E ZMWs at -j 8: 317-321 ms from
+    // the last batch to the exit against 345-369, r06j; CCSX_LAST_CLOSE=0: off)
+    const bool last_close = !(getenv("CCSX_LAST_CLOSE") && atoi(getenv("CCSX_LAST_CLOSE")) == 0);
     // the chunk the input ends in: batches per context (the run ends on its
     // slowest batch; smaller ones let the contexts end together)
     uint32_t last_batches_per_ctx = 1;
@@ -699,7 +703,7 @@ int main(int argc, char **argv)
         // The output waits for the work, not for the release (work_done)
         const bool last = workers_busy.fetch_sub(1) == 1;
         work_done(w);
-        if (!fatal && !last && early_close) {
+        if (!fatal && (!last || last_close) && early_close) {
             ccsx_gpu_close(ctx[w]);
             ctx[w] = nullptr;
         }

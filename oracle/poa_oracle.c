@@ -179,6 +179,31 @@ void opoa_row_kinds(uint64_t *out, int reset)
     if (reset) memset(row_kinds, 0, sizeof row_kinds);
 }
 
+/* Debug statistics: the traceback's predecessor moves by the row distance
+ * they cover (1, 2, 3, 4-8, far row) and M / D kind, and the traceback steps;
+ * summed like row_kinds (tools/row_kinds.py --tb). */
+enum { TB_D1, TB_D2, TB_D3, TB_D4_8, TB_FAR, TB_MOVES_D, TB_STEPS, TB_M4, TB_M5_8, TB_DD1, TB_DDFAR, TB_DDGE2, TB_N };
+static uint64_t tb_moves[TB_N];
+void opoa_tb_moves(uint64_t *out, int reset)
+{
+    memcpy(out, tb_moves, sizeof tb_moves);
+    if (reset) memset(tb_moves, 0, sizeof tb_moves);
+}
+
+static void count_tb_move(const graph_t *G, uint32_t r, uint32_t p, int isD)
+{
+    const uint32_t np = G->poff[r + 1] - G->poff[r];
+    int far = np > 4;
+    for (uint32_t s = 0; s < np; ++s) far |= r - G->pred[G->poff[r] + s] > OPOA_KRING;
+    const uint32_t d = r - p;
+    tb_moves[far ? TB_FAR : d == 1 ? TB_D1 : d == 2 ? TB_D2 : d == 3 ? TB_D3 : TB_D4_8]++;
+    if (isD) tb_moves[TB_MOVES_D]++;
+    if (isD && !far) tb_moves[d == 1 ? TB_DD1 : TB_DDGE2]++;
+    if (isD && far) tb_moves[TB_DDFAR]++;
+    if (!isD && !far && d == 4) tb_moves[TB_M4]++;
+    if (!isD && !far && d > 4) tb_moves[TB_M5_8]++;
+}
+
 static void count_row_kind(const graph_t *G, uint32_t r, int32_t off, int32_t poff, const uint8_t *spill)
 {
     const uint32_t np = G->poff[r + 1] - G->poff[r];
@@ -324,11 +349,14 @@ static void traceback(opoa_t *g, uint32_t m, uint32_t er, uint32_t ej)
         }
         const size_t cell = (size_t)r * W + (size_t)(j - g->roff[r]);
         const uint8_t c = g->code[cell];
+        tb_moves[TB_STEPS]++;
         if (st == 0) {
             const int hc = c & 3;
             if (hc == HC_MPRED) {
                 g->ev[j] = (EV_ALN << 30) | r;
-                r = G->pred[G->poff[r] + g->ms[cell]];
+                const uint32_t p = G->pred[G->poff[r] + g->ms[cell]];
+                count_tb_move(G, r, p, 0);
+                r = p;
                 --j;
             } else if (hc == HC_MSRC) {
                 g->ev[j] = (EV_ALN << 30) | r;
@@ -341,7 +369,9 @@ static void traceback(opoa_t *g, uint32_t m, uint32_t er, uint32_t ej)
             }
         } else if (st == 1) {
             st = (c >> 2) & 1 ? 1 : 0;
-            r = G->pred[G->poff[r] + g->ds[cell]];
+            const uint32_t p = G->pred[G->poff[r] + g->ds[cell]];
+            count_tb_move(G, r, p, 1);
+            r = p;
         } else {
             g->ev[j] = (EV_INS << 30) | r;
             st = (c >> 3) & 1 ? 2 : 0;

@@ -20,7 +20,8 @@
 #   phase:L,P,N[:KCFG] per-ZMW phase cycle split (tools/phase_prof.py) of N ZMWs of L x P
 #   cli:N[:pipe|:fifo] CLI end to end on N config-E ZMWs on stdin, sample vs oracle (tools/cli_stream.py;
 #                      pipe: generator piped in, fifo: output through a FIFO)
-#   shape:N[:J,J...[:REPS]]  the CLI on N config-E ZMWs at -j J bound to J CPUs (the N = 8 per-rank shape)
+#   shape:N[:J,J...[:REPS]]  the CLI on N config-E ZMWs at -j J bound to J CPUs (the N = 8 per-rank shape;
+#                      SHAPE_TAG names the output directory's suffix)
 #   ingest:N           step 0 + prepare alone on N config-E ZMWs (tools/ingest_rate.sh, CPU only)
 #   n2:EZMWS           bench.py through torch.distributed.run with two ranks on the box's GPU
 #   env:NAME=VALUE     export NAME for the following steps (env:NAME= unsets it)
@@ -124,9 +125,10 @@ step() {
       timeout -k 10 1000 python -u tools/cli_stream.py --n "$cfg" $flag --out "$OUT/$tag" > "$OUT/$tag.log" 2>&1
       local rc=$?; tail -5 "$OUT/$tag.log"; return $rc ;;
     shape)  # shape:N:J,J,... -- the CLI on N config-E ZMWs at -j J bound to J CPUs (tools/rank_shape.py)
-      timeout -k 10 900 python -u tools/rank_shape.py --n "$cfg" --jobs "${k:-2,4,8,16}" --repeat "${x:-1}" --out "$OUT/shape_$cfg" \
-        > "$OUT/shape_$cfg.log" 2>&1
-      local rc=$?; tail -6 "$OUT/shape_$cfg.log"; return $rc ;;
+      local d="$OUT/shape_$cfg${SHAPE_TAG:+_$SHAPE_TAG}"
+      timeout -k 10 900 python -u tools/rank_shape.py --n "$cfg" --jobs "${k:-2,4,8,16}" --repeat "${x:-1}" --out "$d" \
+        > "$d.log" 2>&1
+      local rc=$?; tail -6 "$d.log"; return $rc ;;
     ingest)  # ingest:N -- step 0 (one reader) + prepare rate on N config-E ZMWs from a file (CPU only)
       timeout -k 10 900 bash tools/ingest_rate.sh "$cfg" 16 "gpurun_out/$TAG" > "$OUT/ingest_$cfg.log" 2>&1
       local rc=$?; tail -2 "$OUT/ingest_$cfg.log"; return $rc ;;

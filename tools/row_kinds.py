@@ -27,6 +27,7 @@ def main() -> None:
     ap.add_argument("--config", default="E")
     ap.add_argument("--n", type=int, default=24)
     ap.add_argument("--json")
+    ap.add_argument("--tb", action="store_true", help="also the traceback's predecessor moves by row distance")
     a = ap.parse_args()
     import bench
     from oracle.oracle import Poa, lib, prepare as oracle_prepare
@@ -38,6 +39,10 @@ def main() -> None:
         [bench.E_LAUNCH_HOLE0 + i for i in range(a.n)]
     out = (C.c_uint64 * len(KINDS))()
     L.opoa_row_kinds(out, 1)
+    TB = ["d1", "d2", "d3", "d4_8", "far", "moves_D", "steps", "M_d4", "M_d5_8", "D_d1", "D_far", "D_d2_8"]
+    tbo = (C.c_uint64 * len(TB))()
+    L.opoa_tb_moves.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    L.opoa_tb_moves(tbo, 1)
     p = Poa()
     for h in holes:
         Ls, passes = bench.zmw_shape(cfg, h)
@@ -48,6 +53,13 @@ def main() -> None:
     rows = sum(cnt[k] for k in KINDS if k != "spill")
     res = {"config": a.config, "zmws": len(holes), "rows": rows,
            "frac": {k: round(cnt[k] / rows, 4) for k in KINDS}}
+    if a.tb:
+        L.opoa_tb_moves(tbo, 1)
+        t = dict(zip(TB, [int(x) for x in tbo]))
+        mv = sum(t[k] for k in TB[:5])
+        res["tb"] = {"steps": t["steps"], "moves": mv, "moves_D": t["moves_D"],
+                     "frac": {k: round(t[k] / max(mv, 1), 5) for k in TB[:5]},
+                     "by_kind": {k: t[k] for k in TB[7:]}}
     print(json.dumps(res))
     if a.json:
         with open(a.json, "w") as f:
