@@ -47,14 +47,14 @@ KCFGS = [(n, [f"-DCCSX_KCFG={n}", f"-DCCSX_LAUNCH=ccsx_launch_zmw_{n}", f"-DCCSX
                       # traceback block and 96 VGPRs: ~5.5 KB of LDS, 20 workgroups per CU
                       ("solo16", ["-DCCSX_RINGA=8", "-DCCSX_BLK=8", "-DCCSX_RING=8", "-DCCSX_HELPERS=0",
                                   "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0", "-DCCSX_PRIO_TB=1", "-DCCSX_PRIO_MG=1",
-                                  "-DCCSX_RING16", "-DCCSX_TB_ROWS=16",
+                                  "-DCCSX_RING16", "-DCCSX_TB_ROWS=32",
                                   "-DCCSX_WAVES_PER_EU=5"]),
                       # solo16 at 80 VGPRs: 24 workgroups per CU, for slices of few-segment ZMWs
                       # (config E: 16,384 ZMWs per launch 582 -> 569 ms; config D's 30 passes keep
                       # solo16: 314 vs 319 ms, r06c)
                       ("solo16w", ["-DCCSX_RINGA=8", "-DCCSX_BLK=8", "-DCCSX_RING=8", "-DCCSX_HELPERS=0",
                                    "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0", "-DCCSX_PRIO_TB=1", "-DCCSX_PRIO_MG=1",
-                                   "-DCCSX_RING16", "-DCCSX_TB_ROWS=16",
+                                   "-DCCSX_RING16", "-DCCSX_TB_ROWS=32",
                                    "-DCCSX_WAVES_PER_EU=6"])]]
 
 

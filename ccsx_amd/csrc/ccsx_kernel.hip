@@ -14,8 +14,8 @@
 // [-3, 4] is three immediate-offset reads.  Rows needed more than kRing rows
 // later are spilled to HBM.  Helper waves 1 and 2 follow one lockstep block
 // of kBlkAB rows behind, recompute each cell's decision bits from the ring
-// and store 16-bit cell records (code | D-ext | I-ext | M tag | D tag) to
-// HBM, 256 B per row, rotated per row for the traceback's LDS banks.
+// and store 8-bit cell records (code | D-ext | I-ext | M tag | D tag) to HBM,
+// 128 B per row, rotated per row for the traceback's LDS banks (row_record).
 // Traceback (SPEC.md §4) walks those records on wave 0 from 32-row blocks
 // LDS-DMA'd double-buffered; merge (§5) and the column counts (§6) run on all
 // three waves.  The same source builds four configurations (ccsx_layout.h
@@ -229,6 +229,7 @@ struct Z {
     int cur;
     uint32_t R, E;
     int32_t status;
+    uint32_t nfar;       // DP: this wave's next far slot record (helper h: h, h + 2, ...)
     unsigned long long cells;
     Prof pf;
 };
@@ -437,45 +438,59 @@ __device__ __forceinline__ uint32_t win_codes(uint32_t win, int32_t off, int32_t
     return win >> ((((uint32_t)off + 2u * lane_id()) & 3u) * 2u + 2u * (uint32_t)d);
 }
 
-// per lane: row r0+lane's info and first four predecessors (the one-wave
-// objects: the four predecessors' row distances, 8 bits each, in dpk -- a
-// row without the far flag has every predecessor within kRing rows -- two
-// VGPRs per 64-row window instead of five)
+// The 8-bit cell record (row_record): code (bits 0-1) | D-ext (2) | I-ext (3)
+// | M tag (4-6) | D tag (7).  M tag: -d as 3-bit two's complement for the
+// predecessor d = 1..4 rows back, else (0..3) an escape; D tag: 1 = row r - 1,
+// else an escape.  An escape's distance d - 1 sits in the row's tag plane (D:
+// 4 bits per cell; M too where the ring is longer than 8 rows -- on the
+// others an M escape is (-d) & 7 = 8 - d for d = 5..8).  Rows flagged far
+// carry neither: their slots go to a far slot record.  The tag byte of a
+// predecessor d rows back (what pred_fold keeps per cell; d <= kRing on rows
+// not flagged far): M tag << 4 | D tag << 7 | (d - 1).  merge computes them
+// into the DP's row records (RowPre::dpk): in the DP the arithmetic took ~9
+// scalar instructions per predecessor, config D +4 % on the scalar unit
+// (r06m).  Traceback: 98.8 % of config-E predecessor moves go 1-3 rows back,
+// 0.5 % 4-8 (tools/row_kinds.py --tb).
+__device__ __forceinline__ uint32_t tagb(uint32_t d)
+{
+    // d = 8, 1, 2, 3 | 4, 5, 6, 7 by d & 3; beyond 8 rows: M escape 0, D escape
+    return d > 8u ? d - 1u : ((d & 4u) ? 0x16253443u : 0x5261F007u) >> ((d & 3u) * 8u);
+}
+constexpr uint32_t kTagPrev = 0xF0u;  // tagb(1): the previous row
+static_assert(kRing <= 16, "tag bytes hold distances up to 16");
+
+// per lane: row r0+lane's info and the tag bytes of its first four
+// predecessors (merge writes them: the distance d - 1 in the low nibble, so a
+// row without the far flag -- every predecessor within kRing rows, at most
+// four -- finds its predecessors too; two VGPRs per 64-row window)
 struct RowPre {
-    uint32_t info, po, p0, p1, p2, p3, dpk;
+    uint32_t info, dpk;
 };
 // row info bits: base (0-1) | spill (2: a successor lies > kRing rows ahead)
 // | chain (3: the only predecessor is the previous row) | far (4: a
 // predecessor lies > kRing rows back or there are > 4) | np << 8
 constexpr uint32_t kInfoSpill = 4u, kInfoChain = 8u, kInfoFar = 16u;
 
+// tag byte k (< 4) of row r = r0 + li (bits above the byte: the next slots')
+__device__ __forceinline__ uint32_t row_tag(const RowPre &W, int li, int k)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)W.dpk, li) >> (8 * k);
+}
+
 // predecessor k (< 4) of row r = r0 + li of a non-far row, from the window
 __device__ __forceinline__ uint32_t row_pred(const RowPre &W, uint32_t r, int li, int k)
 {
-    if constexpr (kHelpers == 0) {
-        const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)W.dpk, li);
-        return r - ((dk >> (8 * k)) & 255u);
-    }
-    const uint32_t v = k == 0 ? W.p0 : k == 1 ? W.p1 : k == 2 ? W.p2 : W.p3;
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, li);
+    return r - 1u - (row_tag(W, li, k) & 15u);
 }
 
-// the DP's row records (written by merge): coalesced, no dependent loads
+// the DP's row records {info, tag bytes} (written by merge): coalesced, no
+// dependent loads
 __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o)
 {
     const uint32_t n = r0 < z.R ? z.R - r0 : 0u;
     const uint32_t sp = __builtin_amdgcn_raw_buffer_load_b8(brsrc(P<const uint8_t>(z, z.L.spf) + r0, n), lane_id(), 0, 0);
-    if constexpr (kHelpers == 0) {
-        // {info, dpk} (merge writes them so on the one-wave objects)
-        const v2u q = __builtin_amdgcn_raw_buffer_load_b64(brsrc(P<const uint4>(z, z.L.rrec) + r0, n * 16),
-                                                           lane_id() * 16, 0, 0);
-        o.info = q.x | (sp ? kInfoSpill : 0u), o.dpk = q.y;
-        return;
-    }
-    const v4u q = __builtin_amdgcn_raw_buffer_load_b128(brsrc(P<const uint4>(z, z.L.rrec) + r0, n * 16),
-                                                        lane_id() * 16, 0, 0);
-    o.info = q.x | (sp ? kInfoSpill : 0u), o.p0 = q.y, o.p1 = q.z, o.p2 = q.w;
-    o.p3 = __builtin_amdgcn_raw_buffer_load_b32(brsrc(P<const uint32_t>(z, z.L.rp3) + r0, n * 4), lane_id() * 4, 0, 0);
+    const v2u q = __builtin_amdgcn_raw_buffer_load_b64(brsrc(P<const uint2>(z, z.L.rrec) + r0, n * 8), lane_id() * 8, 0, 0);
+    o.info = q.x | (sp ? kInfoSpill : 0u), o.dpk = q.y;
 }
 
 // ----------------------------------------------------------------------------
@@ -507,12 +522,12 @@ __device__ __forceinline__ void prefetch_recs(const Z &z, uint32_t r0, RowPre &o
 //    always below the H' it extends);
 //  * free-end candidates are tracked on H' for the same reason.
 // ----------------------------------------------------------------------------
-// Cell records (16 bits, cell t of row r) sit in the row's 256 B at byte
-// (2 t + tb_rot(r)) & 255: each row is rotated by two words per row of its
-// 32-row traceback block, so the traceback's window fill -- 32 lanes reading
-// the same column of 32 consecutive rows -- spreads over the LDS banks instead
-// of hitting one (a 256 B pitch is a multiple of the 32-bank width).
-__device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 8u; }
+// Cell records (8 bits, cell t of row r) sit in the row's 128 B at byte (t +
+// tb_rot(r)) & 127: each row is rotated by one word per row of its 32-row
+// traceback block, so the traceback's window fill -- 32 lanes reading the
+// same column of 32 consecutive rows -- spreads over the LDS banks instead of
+// hitting one (a 128 B pitch is a multiple of the bank width).
+__device__ __forceinline__ uint32_t tb_rot(uint32_t r) { return (r & 31u) * 4u; }
 
 constexpr int kHc = 4, kDc = 140;  // word of cell 0 of H / D in a ring row
 constexpr int32_t kNegH = kNeg - kO - kE;
@@ -573,9 +588,10 @@ struct PredAcc {
     uint32_t ms0, ms1, ds0, ds1, dx0, dx1;
 };
 
-// SLOTS: also track, per cell, the tag of the predecessor that gave Mh and D
-// (first in predecessor order on ties, SPEC.md §3.2) and D's ext bit; the
-// tag is the row distance r - p (or the slot index on rows flagged far)
+
+// SLOTS: also track, per cell, the tag byte of the predecessor that gave Mh
+// and D (first in predecessor order on ties, SPEC.md §3.2) and D's ext bit
+// (rows flagged far: the tag is the slot index)
 template <bool SLOTS>
 __device__ __forceinline__ void pred_fold(PredAcc &A, uint32_t s, uint32_t tag, int32_t hA, int32_t hB, int32_t hC,
                                           int32_t dB, int32_t dC)
@@ -624,7 +640,7 @@ __device__ __forceinline__ void pred_cells(const RingT *row, int32_t sh, int lan
 template <bool SLOTS>
 __device__ __forceinline__ void pred_terms(const RingT *ring, uint32_t r, int32_t off, uint32_t np, uint32_t p0,
                                            uint32_t p1, uint32_t p2, uint32_t p3, int32_t o0, int32_t o1, int32_t o2,
-                                           int32_t o3, int lane, PredAcc &A)
+                                           int32_t o3, uint32_t tg, int lane, PredAcc &A)
 {
     const int32_t s0 = off - o0, s1 = off - o1, s2 = off - o2, s3 = off - o3;
     const bool inr = (uint32_t)(s0 + 3) <= 7u && (np < 2 || (uint32_t)(s1 + 3) <= 7u) &&
@@ -644,25 +660,25 @@ __device__ __forceinline__ void pred_terms(const RingT *ring, uint32_t r, int32_
         const int32_t c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
         const int32_t e0 = b2[0], e1 = b2[1], e2 = b2[2], e3 = b2[dd], e4 = b2[dd + 1];
         const int32_t g0 = b3[0], g1 = b3[1], g2 = b3[2], g3 = b3[dd], g4 = b3[dd + 1];
-        pred_fold<SLOTS>(A, 0, r - p0, a0, a1, a2, a3, a4);
-        if (np > 1) pred_fold<SLOTS>(A, 1, r - p1, c0, c1, c2, c3, c4);
-        if (np > 2) pred_fold<SLOTS>(A, 2, r - p2, e0, e1, e2, e3, e4);
-        if (np > 3) pred_fold<SLOTS>(A, 3, r - p3, g0, g1, g2, g3, g4);
+        pred_fold<SLOTS>(A, 0, tg, a0, a1, a2, a3, a4);
+        if (np > 1) pred_fold<SLOTS>(A, 1, tg >> 8, c0, c1, c2, c3, c4);
+        if (np > 2) pred_fold<SLOTS>(A, 2, tg >> 16, e0, e1, e2, e3, e4);
+        if (np > 3) pred_fold<SLOTS>(A, 3, tg >> 24, g0, g1, g2, g3, g4);
     } else {
         int32_t hA, hB, hC, dB, dC;
         pred_cells(ring + (p0 % kRingA) * kRowW, s0, lane, hA, hB, hC, dB, dC);
-        pred_fold<SLOTS>(A, 0, r - p0, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, 0, tg, hA, hB, hC, dB, dC);
         if (np > 1) {
             pred_cells(ring + (p1 % kRingA) * kRowW, s1, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 1, r - p1, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 1, tg >> 8, hA, hB, hC, dB, dC);
         }
         if (np > 2) {
             pred_cells(ring + (p2 % kRingA) * kRowW, s2, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 2, r - p2, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 2, tg >> 16, hA, hB, hC, dB, dC);
         }
         if (np > 3) {
             pred_cells(ring + (p3 % kRingA) * kRowW, s3, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 3, r - p3, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 3, tg >> 24, hA, hB, hC, dB, dC);
         }
     }
 }
@@ -672,7 +688,7 @@ __device__ __forceinline__ void pred_terms(const RingT *ring, uint32_t r, int32_
 // [-3, 4], else bounds-checked per cell
 template <int NP, bool SLOTS>
 __device__ __forceinline__ void pred_terms_n(const RingT *ring, uint32_t r, int32_t off, uint32_t p0, uint32_t p1,
-                                             int32_t o0, int32_t o1, int lane, PredAcc &A)
+                                             int32_t o0, int32_t o1, uint32_t tg, int lane, PredAcc &A)
 {
     const int32_t s0 = off - o0, s1 = off - o1;
     // (one unsigned max: fewer scalar compares and selects than an &&)
@@ -685,15 +701,15 @@ __device__ __forceinline__ void pred_terms_n(const RingT *ring, uint32_t r, int3
         const int32_t a0 = b0[0], a1 = b0[1], a2 = b0[2], a3 = b0[dd], a4 = b0[dd + 1];
         int32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
         if (NP > 1) c0 = b1[0], c1 = b1[1], c2 = b1[2], c3 = b1[dd], c4 = b1[dd + 1];
-        pred_fold<SLOTS>(A, 0, r - p0, a0, a1, a2, a3, a4);
-        if (NP > 1) pred_fold<SLOTS>(A, 1, r - p1, c0, c1, c2, c3, c4);
+        pred_fold<SLOTS>(A, 0, tg, a0, a1, a2, a3, a4);
+        if (NP > 1) pred_fold<SLOTS>(A, 1, tg >> 8, c0, c1, c2, c3, c4);
     } else {
         int32_t hA, hB, hC, dB, dC;
         pred_cells(ring + (p0 % kRingA) * kRowW, s0, lane, hA, hB, hC, dB, dC);
-        pred_fold<SLOTS>(A, 0, r - p0, hA, hB, hC, dB, dC);
+        pred_fold<SLOTS>(A, 0, tg, hA, hB, hC, dB, dC);
         if (NP > 1) {
             pred_cells(ring + (p1 % kRingA) * kRowW, s1, lane, hA, hB, hC, dB, dC);
-            pred_fold<SLOTS>(A, 1, r - p1, hA, hB, hC, dB, dC);
+            pred_fold<SLOTS>(A, 1, tg >> 8, hA, hB, hC, dB, dC);
         }
     }
 }
@@ -856,14 +872,14 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
             hA = S.H1, hB = wave_shl1(kNegH, S.H0), hC = wave_shl1(kNegH, S.H1);
             dB = wave_shl1(kNeg, S.D0), dC = wave_shl1(kNeg, S.D1);
         }
-        pred_fold<SLOTS>(A, 0, 1u, hA, hB, hC, dB, dC);  // the predecessor is row r - 1
+        pred_fold<SLOTS>(A, 0, kTagPrev, hA, hB, hC, dB, dC);  // the predecessor is row r - 1
     } else if (np == 1) {
         kind = 2;
         const uint32_t p0 = row_pred(S.W.cur, r, li, 0);
         const int32_t o0 = __builtin_amdgcn_readlane(S.vOff, (int)(p0 & 63u));
         const int32_t k0 = __builtin_amdgcn_readlane(S.vKey, (int)(p0 & 63u));
         off = min(max(o0 + 127 - (k0 & 127) + 1 - kW / 2, 0), lim);
-        pred_terms_n<1, SLOTS>(ring, r, off, p0, p0, o0, o0, lane, A);
+        pred_terms_n<1, SLOTS>(ring, r, off, p0, p0, o0, o0, SLOTS ? row_tag(S.W.cur, li, 0) : 0u, lane, A);
     } else if (np == 2) {
         kind = 3;
         const uint32_t p0 = row_pred(S.W.cur, r, li, 0);
@@ -876,7 +892,7 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
         const bool second = (k1 >> 7) > (k0 >> 7);
         const int32_t ko = second ? k1 : k0, oo = second ? o1 : o0;
         off = min(max(oo + 127 - (ko & 127) + 1 - kW / 2, 0), lim);
-        pred_terms_n<2, SLOTS>(ring, r, off, p0, p1, o0, o1, lane, A);
+        pred_terms_n<2, SLOTS>(ring, r, off, p0, p1, o0, o1, SLOTS ? row_tag(S.W.cur, li, 0) : 0u, lane, A);
     } else {
         const uint32_t p0 = row_pred(S.W.cur, r, li, 0);
         const uint32_t p1 = row_pred(S.W.cur, r, li, 1);
@@ -898,7 +914,8 @@ __device__ __forceinline__ void dpA_cold(const Z &z, const AState &S, uint32_t r
             if (np > 3 && (k3 >> 7) > bm) bm = k3 >> 7, barg = o3 + 127 - (k3 & 127);
             off = min(max(barg + 1 - kW / 2, 0), lim);
         }
-        pred_terms<SLOTS>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
+        pred_terms<SLOTS>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, SLOTS ? row_tag(S.W.cur, li, 0) : 0u, lane,
+                          A);
     }
     off_o = off;
 }
@@ -1110,20 +1127,56 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
         far_terms<true>(z, r, np, vOff, 0, 0, false, o, A);
         return;
     }
-    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
-    const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p1, li);
+    const uint32_t tg = row_tag(S.W.cur, li, 0);
+    const uint32_t p0 = r - 1u - (tg & 15u), p1 = r - 1u - ((tg >> 8) & 15u);
     const int32_t o0 = __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
     const int32_t o1 = __builtin_amdgcn_readlane(vOff, (int)(p1 & 63u));
     if (np == 2) {
-        pred_terms_n<2, true>(ring, r, off, p0, p1, o0, o1, lane, A);
+        pred_terms_n<2, true>(ring, r, off, p0, p1, o0, o1, tg, lane, A);
     } else if (np == 1) {
-        pred_terms_n<1, true>(ring, r, off, p0, p0, o0, o0, lane, A);
+        pred_terms_n<1, true>(ring, r, off, p0, p0, o0, o0, tg, lane, A);
     } else {
-        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p2, li);
-        const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p3, li);
+        const uint32_t p2 = r - 1u - ((tg >> 16) & 15u), p3 = r - 1u - ((tg >> 24) & 15u);
         const int32_t o2 = __builtin_amdgcn_readlane(vOff, (int)(p2 & 63u));
         const int32_t o3 = __builtin_amdgcn_readlane(vOff, (int)(p3 & 63u));
-        pred_terms<true>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, lane, A);
+        pred_terms<true>(ring, r, off, np, p0, p1, p2, p3, o0, o1, o2, o3, tg, lane, A);
+    }
+}
+
+// The records beside a row's cell bytes: a far row's slot record (u16 M / D
+// slot per cell, its index in word 0 of the row's tag-plane row), or, for a
+// row with a predecessor more than one row back, its tag plane: the D
+// distance - 1 per cell, 4 bits (and the M one beside it, a byte per cell,
+// where the ring is longer than 8 rows).  A chain row needs neither.
+// (Buffer stores: a store through a generic pointer is a flat store, which
+// also counts in lgkmcnt, so the next row's wait on its ring reads would wait
+// for it to reach memory.)
+__device__ __forceinline__ void row_slots(Z &z, uint32_t r, uint32_t info, const PredAcc &A)
+{
+    const uint32_t lane = lane_id();
+    if (info & kInfoFar) {
+        const uint32_t fs = z.nfar;
+        z.nfar += (uint32_t)kHelperStep;
+        if (fs < z.d.wcap) {
+            // (rare: buffer stores, whose descriptors cost scalar work but no VGPRs)
+            const auto fr = brsrc(PX<uint8_t>(z, kExtWtag), z.d.wcap * (kW * 4u));
+            __builtin_amdgcn_raw_buffer_store_b64(v2u{A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16)}, fr,
+                                                  fs * (kW * 4u) + lane * 8u, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(fs, brsrc(P<uint8_t>(z, z.L.dsl), z.R * kRecRow),
+                                                  lane == 0 ? r * kRecRow : ~0u, 0, 0);
+        } else {
+            z.status = kErrSpill;  // (re-run with full caps: a far slot record per row)
+        }
+    } else if (!(info & kInfoChain)) {
+        const auto tpr = brsrc(P<uint8_t>(z, z.L.dsl), z.R * kRecRow);
+        if constexpr (kRing <= 8) {
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((A.ds0 & 15u) | ((A.ds1 & 15u) << 4)), tpr, r * kRecRow + lane, 0,
+                                                 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b16(
+                (unsigned short)((A.ms0 & 15u) | ((A.ds0 & 15u) << 4) | ((A.ms1 & 15u) << 8) | ((A.ds1 & 15u) << 12)), tpr,
+                r * kRecRow + lane * 2u, 0, 0);
+        }
     }
 }
 
@@ -1132,8 +1185,7 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
 // the helpers' dpB_tail (values recomputed from the ring) and the solo
 // dpS_row (values the wave holds) share it.  mp / d: M came from a
 // predecessor / D beat M, per cell; X = H' + 2 t; Pex = the insertion scan's
-// exclusive prefix max.  maybe_wide: the row may have more than 63
-// predecessors (its slots also go to the wide slot records).
+// exclusive prefix max.  cold: the row may need row_slots (info: its flags).
 // a row's position in its DP block, for the solo wave's row bookkeeping
 struct RowX {
     uint32_t chn;    // dpS_row: 1 if the row is a plain chain row (one predecessor, r - 1, no far / spill flags)
@@ -1144,13 +1196,13 @@ struct RowX {
 };
 __device__ __forceinline__ RowX row_x(uint32_t r, uint32_t m)
 {
-    return RowX{1u, tb_rot(r), 0u, r * 256u, -2 * (int32_t)m - 1};
+    return RowX{1u, tb_rot(r), 0u, r * kRecRow, -2 * (int32_t)m - 1};
 }
 
 template <bool FULL, bool TRACK_OFF = true>
 __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, int32_t &bOff,
                                            const __amdgpu_buffer_rsrc_t &rc, uint32_t r, uint32_t m, int32_t lim,
-                                           int32_t off, uint32_t np, bool maybe_wide, const PredAcc &A, const LaneK &c,
+                                           int32_t off, uint32_t info, bool cold, const PredAcc &A, const LaneK &c,
                                            bool mp0, bool mp1, bool d0, bool d1, int32_t hp0, int32_t hp1, int32_t X0,
                                            int32_t X1, int32_t Pex, const RowX &x)
 {
@@ -1161,13 +1213,9 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
     const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
     const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
-    uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
-    uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
-    if (maybe_wide && __builtin_expect(np > 63u, 0)) {
-        // wide slot record of row r: u16 M / D slots per cell
-        reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
-            make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
-    }
+    uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 & 0x70u) | (A.ds0 & 0x80u);
+    uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 & 0x70u) | (A.ds1 & 0x80u);
+    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, r, info, A);
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
     // H' at j = m - 1
     const int32_t eb = (off << 1) + x.em1;
@@ -1200,7 +1248,8 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
     // rotated by tb_rot(r) words within the row (the traceback's LDS bank skew)
     // (the block's base as the store's scalar offset, the row's in the
     // instruction's offset field)
-    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, (((uint32_t)lane * 4u + x.rot) & 255u) + x.ioff, x.sbase, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w0 | (w1 << 8)), rc, (((uint32_t)lane * 2u + x.rot) & 127u) + x.ioff,
+                                          x.sbase, 0);
 }
 
 // row_record for the one-wave DP (dpS_row): the same records and free-end
@@ -1211,8 +1260,8 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
 // and a shift-or per row)
 template <bool FULL>
 __device__ __forceinline__ void row_record_solo(Z &z, int32_t &bE, uint32_t &bKey, const __amdgpu_buffer_rsrc_t &rc,
-                                                uint32_t r, uint32_t m, int32_t lim, int32_t off, uint32_t np,
-                                                bool maybe_wide, const PredAcc &A, const LaneK &c, bool mp0, bool mp1,
+                                                uint32_t r, uint32_t m, int32_t lim, int32_t off, uint32_t info,
+                                                bool cold, const PredAcc &A, const LaneK &c, bool mp0, bool mp1,
                                                 bool d0, bool d1, int32_t hp0, int32_t hp1, int32_t X0, int32_t X1,
                                                 int32_t xm, int32_t Pex, int32_t ex1, const RowX &x)
 {
@@ -1222,12 +1271,9 @@ __device__ __forceinline__ void row_record_solo(Z &z, int32_t &bE, uint32_t &bKe
     const uint32_t iext0 = Pex > X1L ? 8u : 0u, iext1 = Pex > X0 ? 8u : 0u;
     const uint32_t hc0 = i0 ? HC_INS : d0 ? HC_DEL : mp0 ? HC_MPRED : HC_MSRC;
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
-    uint32_t w0 = hc0 | A.dx0 | iext0 | ((A.ms0 & 63u) << 4) | ((A.ds0 & 63u) << 10);
-    uint32_t w1 = hc1 | A.dx1 | iext1 | ((A.ms1 & 63u) << 4) | ((A.ds1 & 63u) << 10);
-    if (maybe_wide && __builtin_expect(np > 63u, 0)) {
-        reinterpret_cast<uint2 *>(PX<uint8_t>(z, kExtWtag) + (size_t)r * (kW * 4))[lane] =
-            make_uint2(A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16));
-    }
+    uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 & 0x70u) | (A.ds0 & 0x80u);
+    uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 & 0x70u) | (A.ds1 & 0x80u);
+    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, r, info, A);
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1 = X + eb
     // (x.em1 carries -kXBias), and H' at j = m - 1 (+3)
     const int32_t eb = (off << 1) + x.em1;
@@ -1256,7 +1302,8 @@ __device__ __forceinline__ void row_record_solo(Z &z, int32_t &bE, uint32_t &bKe
         const int32_t e01 = c1 ? e1 : e0;
         if (e01 > bE) bE = e01, bKey = r * 2 + (c1 ? 1u : 0u);
     }
-    __builtin_amdgcn_raw_buffer_store_b32(w0 | (w1 << 16), rc, (((uint32_t)lane * 4u + x.rot) & 255u) + x.ioff, x.sbase, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w0 | (w1 << 8)), rc, (((uint32_t)lane * 2u + x.rot) & 127u) + x.ioff,
+                                          x.sbase, 0);
 }
 
 // helper wave: everything after the predecessor terms of row r (SPEC.md
@@ -1264,7 +1311,7 @@ __device__ __forceinline__ void row_record_solo(Z &z, int32_t &bE, uint32_t &bKe
 // free-end candidates, the record store
 template <bool FULL>
 __device__ __forceinline__ void dpB_tail(Z &z, BState &S, uint32_t r, uint32_t m, int32_t lim, int32_t off, uint32_t qp,
-                                         uint32_t base, uint32_t np, const PredAcc &A, const LaneK &c)
+                                         uint32_t base, uint32_t info, const PredAcc &A, const LaneK &c)
 {
     const int lane = lane_id();
     const int32_t srcu = c.src0 + kE * off;
@@ -1278,7 +1325,7 @@ __device__ __forceinline__ void dpB_tail(Z &z, BState &S, uint32_t r, uint32_t m
     // insertions (SPEC.md §3.4): the same prefix-max scan as wave 0's
     const int32_t X0 = hp0 + c.L4, X1 = hp1 + c.L4 + 2;
     const int32_t Pex = wave_shr1(kNeg, wave_incl_max(max(X0, X1)));
-    row_record<FULL>(z, S.bE, S.bKey, S.bOff, S.rc, r, m, lim, off, np, true, A, c, mp0, mp1, d0, d1, hp0, hp1, X0, X1,
+    row_record<FULL>(z, S.bE, S.bKey, S.bOff, S.rc, r, m, lim, off, info, true, A, c, mp0, mp1, d0, d1, hp0, hp1, X0, X1,
                      Pex, row_x(r, m));
 }
 
@@ -1303,7 +1350,8 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
     const RingT *dv = reinterpret_cast<const RingT *>(z.lds + kLdsRing) + (r % kRingA) * kRowW + kDc + c.L2;
     PredAcc A;
     A.Dv0 = dv[0], A.Dv1 = dv[1];
-    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)S.W.cur.p0, li);
+    const uint32_t tg = row_tag(S.W.cur, li, 0);
+    const uint32_t p0 = r - 1u - (tg & 15u);
     const int32_t sh = off - __builtin_amdgcn_readlane(vOff, (int)(p0 & 63u));
     if (__builtin_expect(np == 1 && (uint32_t)(sh + 3) <= 7u && !(info & kInfoFar), 1)) {
         // one predecessor in the padded band: its H at t-1, t, t+1; D-ext is
@@ -1317,7 +1365,7 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
         // read cost the near-critical helpers more; tools/gpu_lds_ab.sh r02y)
         const int32_t hA = b[0], hB = b[1], hC = b[2];
         A.Mh0 = hA, A.Mh1 = hB;
-        A.ms0 = A.ms1 = A.ds0 = A.ds1 = r - p0;
+        A.ms0 = A.ms1 = A.ds0 = A.ds1 = tg;
         A.dx0 = A.Dv0 > hB + (kO + kE) ? 4u : 0u;
         A.dx1 = A.Dv1 > hC + (kO + kE) ? 4u : 0u;
         DP_STAMP(kPfSpare2);
@@ -1325,7 +1373,7 @@ __device__ __forceinline__ void dpB_row(Z &z, BState &S, uint32_t r, uint32_t m,
         dpB_cold(z, S, r, info, off, vOff, A);
         DP_STAMP(kPfSpare3);
     }
-    dpB_tail<FULL>(z, S, r, m, lim, off, qp, info & 3u, np, A, c);
+    dpB_tail<FULL>(z, S, r, m, lim, off, qp, info & 3u, info, A, c);
     DP_STAMP(kPfFlush);
 }
 
@@ -1377,7 +1425,7 @@ __device__ __forceinline__ void dp_two_wave(Z &z, uint32_t m, uint32_t &er_out, 
     S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
     S.qn = rd_win16(z, 0, true);
     S.nspill = 0;
-    S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
+    S.W.cur = RowPre{0, 0};
     S.W.nxt = S.W.cur;
     const uint32_t nblk = dp_nblk(z.R);
 #ifdef CCSX_DP_STAMPS
@@ -1428,9 +1476,10 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
     BState S;
     S.bE = INT32_MIN, S.bKey = 0, S.bOff = 0;
     S.wc0 = 0, S.wnc = 2;
-    S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
+    S.W.cur = RowPre{0, 0};
     S.W.nxt = S.W.cur;
-    S.rc = brsrc(z.ws + z.L.codes, z.R * 256u);
+    S.rc = brsrc(z.ws + z.L.codes, z.R * kRecRow);
+    z.nfar = h;
     const uint32_t nblk = dp_nblk(z.R);
 #ifdef CCSX_DP_STAMPS
     unsigned long long t_prev = stamp();
@@ -1575,14 +1624,14 @@ __device__ __forceinline__ void dpS_row(Z &z, AState &S, SolB &B, uint32_t r, in
         S.pArg = off + kW / 2 - (key & 127);
         // decision bits, free-end candidates, record (only a cold row can
         // have more than 63 predecessors)
-        row_record_solo<FULL>(z, B.bE, B.bKey, B.rc, r, m, lim, off, np, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0, X1,
+        row_record_solo<FULL>(z, B.bE, B.bKey, B.rc, r, m, lim, off, info, cold, A, c, mp0, mp1, d0, d1, hp0, hp1, X0, X1,
                               xm, Pex, ex1, x);
     };
     if (__builtin_expect(fast, 1)) {
         // the only predecessor is row r - 1 (tag 1), band moved by 0 or 1:
         // its cells from registers by DPP; D-ext = the D term won strictly
         PredAcc A;
-        A.ms0 = A.ms1 = A.ds0 = A.ds1 = 1u;
+        A.ms0 = A.ms1 = A.ds0 = A.ds1 = kTagPrev;
         int32_t a0, b0, a1, b1;
         // the tail instantiated per band move: no join of the predecessor
         // terms (whose register copies cost ~5 VALU per row; E16k -0.4 %, r04zd)
@@ -1650,7 +1699,7 @@ __device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0,
     static_assert(kRingA % kBlkAB == 0 || kBlkAB % kRingA == 0, "a block's rows take constant ring slots");
     const uint32_t rb = (r0 % (uint32_t)kRingA) * (uint32_t)kRowW;
     // per row of the block: bit i of fm = row r0 + i is a plain chain row;
-    // tb_rot(r0 + i) = tb_rot(r0) + 8 i (r0 is a multiple of kBlkAB)
+    // tb_rot(r0 + i) = tb_rot(r0) + 4 i (r0 is a multiple of kBlkAB)
     static_assert(kBlkAB <= 16 && 32 % kBlkAB == 0, "a block's rows share tb_rot's 32-row period");
     const uint32_t fm = (uint32_t)(S.fmask >> (r0 & 63u));
     const uint32_t rot0 = tb_rot(r0);
@@ -1659,11 +1708,11 @@ __device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0,
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)kBlkAB; ++i)
             dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + (i % (uint32_t)kRingA) * kRowW,
-                          RowX{(fm >> i) & 1u, rot0 + 8u * i, 256u * i, r0 * 256u, em1});
+                          RowX{(fm >> i) & 1u, rot0 + 4u * i, kRecRow * i, r0 * kRecRow, em1});
     } else {
         for (uint32_t i = 0; r0 + i < R; ++i)
             dpS_row<FULL>(z, S, B, r0 + i, lim, m, c, rb + (i % (uint32_t)kRingA) * kRowW,
-                          RowX{(fm >> i) & 1u, rot0 + 8u * i, 256u * i, r0 * 256u, em1});
+                          RowX{(fm >> i) & 1u, rot0 + 4u * i, kRecRow * i, r0 * kRecRow, em1});
     }
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
     if ((r0 & 15u) == 16u - kBlkAB || rend == R) {
@@ -1694,11 +1743,12 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     S.pOff = 0, S.pArg = 0, S.vOff = 0, S.vKey = 0, S.ring = 0;
     S.qn = rd_win16(z, 0, true);
     S.nspill = 0;
-    S.W.cur = RowPre{0, 0, 0, 0, 0, 0};
+    S.W.cur = RowPre{0, 0};
     S.W.nxt = S.W.cur;
     SolB B;
     B.bE = INT32_MIN, B.bKey = 0;
-    B.rc = brsrc(z.ws + z.L.codes, z.R * 256u);
+    B.rc = brsrc(z.ws + z.L.codes, z.R * kRecRow);
+    z.nfar = 0;
     const uint32_t nblk = dp_nblk(z.R);
     for (uint32_t b = 0; b < nblk && !z.status; ++b) {
         if (z.hbm && z.wpend) {
@@ -1815,27 +1865,37 @@ __device__ __forceinline__ void dp_align(Z &z, uint32_t m, uint32_t &er_out, uin
 
 // ----------------------------------------------------------------------------
 // SPEC.md §4: traceback into one event per read base.  The wave walks the
-// 16-bit cell records of the two-wave DP (code | M tag << 4 | D tag << 10)
-// backwards in 32-row blocks staged in LDS (the next block is loaded while
-// the current one is walked).  One uniform ds_read per step; the band
-// offsets of the current and previous block sit in one VGPR (readlane);
-// events collect in a VGPR, lane j & 63, stored 64 at a time.
+// 8-bit cell records of the DP (row_record: code | D-ext | I-ext | M tag | D
+// tag) backwards in blocks of rows staged in LDS by DMA.  The band offsets of
+// the staged block sit in one VGPR (readlane); events collect in a VGPR,
+// lane j & 63, stored 64 at a time.
 // ----------------------------------------------------------------------------
-// rows per staged record block: 32, or 16 where the ring area is the int16
-// one (solo16: one 16-row block, 4 KiB, fits the 4,352 B area; the window
-// walk below uses lanes 0-15 of each 32-lane half then)
+// rows per staged record block: 32, or 16 (the int16-ring objects: two 16-row
+// blocks of 2 KiB, the next one loaded while the current one is walked, in
+// the 4,352 B ring area)
 #ifndef CCSX_TB_ROWS
 #define CCSX_TB_ROWS 32
 #endif
 constexpr uint32_t kTbRows = CCSX_TB_ROWS;
 static_assert(kTbRows == 32 || kTbRows == 16, "record blocks of 16 or 32 rows");
-constexpr uint32_t kTbBufWords = kTbRows * 64;  // kTbRows rows x 256 B
+constexpr uint32_t kTbBufWords = kTbRows * kRecRow / 4;  // kTbRows rows x 128 B
 // record blocks staged at once: two (the next block's DMA overlaps the walk
-// of the current one) where the DP ring area holds them, else one (the solo
-// configuration's 8-row ring: a block switch waits for its DMA, which the
-// other ZMWs resident on the SIMD cover)
-constexpr uint32_t kTbBufs = (uint32_t)kRingWords >= 2 * kTbBufWords + 128 ? 2u : 1u;
-constexpr uint32_t kTbMeta = kTbBufs * kTbBufWords;  // LDS word of the blocks' row meta (64 words per buffer)
+// of the current one) where the DP ring area holds them, else one (a block
+// switch waits for its DMA, which the other ZMWs resident on the SIMD cover);
+// after the blocks, 32 row meta words per buffer
+#ifdef CCSX_TB_BUFS
+constexpr uint32_t kTbBufs = CCSX_TB_BUFS;
+#else
+constexpr uint32_t kTbBufs = (uint32_t)kRingWords >= 2 * (kTbBufWords + 32) ? 2u : 1u;
+#endif
+// the blocks' tag-plane rows staged beside them where the area holds both (the
+// latency objects, whose single ZMW per SIMD would otherwise wait ~2 us on
+// HBM for each escape on its serial walk; the one-wave objects' other ZMWs
+// cover those waits)
+constexpr bool kTbTags = (uint32_t)kRingWords >= kTbBufs * (2 * kTbBufWords + 32);
+constexpr uint32_t kTbTag = kTbBufs * kTbBufWords;  // LDS word of the staged tag-plane rows (kTbTags)
+constexpr uint32_t kTbMeta = (kTbTags ? 2 : 1) * kTbBufs * kTbBufWords;  // LDS word of the row meta (32 words per buffer)
+static_assert(kTbMeta + kTbBufs * 32 <= (uint32_t)kRingWords, "traceback buffers live in the DP ring area");
 
 // Traceback step tables indexed by (state, cell code), state 0 = H, 1 = D,
 // 2 = I; code = hcode | D-ext << 2 | I-ext << 3 (SPEC.md §3.4, §4).
@@ -1861,101 +1921,137 @@ constexpr uint64_t tb_table(uint32_t st, bool act)
 }
 constexpr uint64_t kTbAct[3] = {tb_table(0, true), tb_table(1, true), tb_table(2, true)};
 constexpr uint64_t kTbNext[3] = {tb_table(0, false), tb_table(1, false), tb_table(2, false)};
-static_assert(kTbBufs * (kTbBufWords + 64) <= (uint32_t)kRingWords, "traceback buffers live in the DP ring area");
 
-// LDS-DMA of 32-row block bi into buffer buf: records (8 KB) and the row
-// meta words (band offset | far << 31); the data bypass VGPRs, so nothing in
-// the walk waits on them until the block is entered (explicit s_waitcnt)
+// LDS-DMA of block bi into buffer buf: records (kTbRows x 128 B) and the row
+// meta words (band offset | far << 31) of 32 rows; the data bypass VGPRs, so
+// nothing in the walk waits on them until the block is entered (explicit
+// s_waitcnt)
 __device__ __forceinline__ void tb_dma(const Z &z, uint32_t bi, uint32_t buf)
 {
     const uint32_t lane = lane_id();
-    const uint8_t *src = z.ws + z.L.codes + (size_t)bi * kTbRows * 256 + lane * 16u;
+    const uint8_t *src = z.ws + z.L.codes + (size_t)bi * kTbRows * kRecRow + lane * 16u;
     int32_t *dst = z.lds + buf * kTbBufWords;
 #pragma unroll
-    for (int k = 0; k < (int)kTbRows / 4; ++k)
+    for (int k = 0; k < (int)(kTbRows * kRecRow / 1024); ++k)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(src + k * 1024), dst + k * 256, 16, 0, 0);
+    if constexpr (kTbTags) {
+        const uint8_t *tsrc = z.ws + z.L.dsl + (size_t)bi * kTbRows * kRecRow + lane * 16u;
+#pragma unroll
+        for (int k = 0; k < (int)(kTbRows * kRecRow / 1024); ++k)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(tsrc + k * 1024),
+                                             z.lds + kTbTag + buf * kTbBufWords + k * 256, 16, 0, 0);
+    }
     const uint32_t *ms = reinterpret_cast<const uint32_t *>(z.ws + z.L.rmeta) + bi * kTbRows + lane;
-    __builtin_amdgcn_global_load_lds(ms, z.lds + kTbMeta + buf * 64, 4, 0, 0);
+    if (lane < 32u) __builtin_amdgcn_global_load_lds(ms, z.lds + kTbMeta + buf * 32, 4, 0, 0);
 }
 
-// Plain MPRED steps k..3 of an aligned 4-column record window (traceback;
-// columns jw - 1 .. jw - 4 of the staged block's 32 rows): wa holds, at lane
-// l < 32 = block row l, columns jw - 1 (low half) and jw - 2 (high half), wb
-// columns jw - 3 and jw - 4 (tb_win's upper 32 lanes moved down by one
-// v_permlane32_swap), so every step reads its record at lane r - base.  Per
-// step, emit ALN | r at lane j & 63; leave with st = 1, unmoved, when the
-// cell's predecessor lies outside the block (tag >= r - base) or, on the
-// window's last column (j = 0 mod 4), when j completes a 64-base chunk; else
-// j -= 1, r -= tag and, below the last column, read the next record and leave
-// with st = 2 when it is not MPRED.  st = 0: moved past the last column (the
-// caller swaps in the next window).  The walk keeps li = r - base as its own
-// variable and leaves high-half records in place (their tag and code are read
-// at bit 20 / 16), so the dependent chain of a step is s_bfe -> s_sub ->
-// v_readlane; a step is 11 instructions (a 64-lane window with li recomputed
-// and the half shifted down per step took 14).
-// Hand-written: compiled, the multi-exit unrolled loop became a flag-driven
-// state machine of ~35 scalar instructions per step.  (Handling D / I steps
-// inside the window as well measured no faster: tools/gpu_ab.sh r02u.)
-// leave the window walk when the predecessor row lies below the block
-// (tag > li: a step may land on the block's first row)
-#define TBW_LEAVE "s_cmp_gt_u32 %[t], %[li]\n\t"
-__device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t wa, uint32_t wb, uint32_t &r,
+// Plain MPRED steps k..7 of an aligned 8-column record window (traceback;
+// columns jw - 1 .. jw - 8 of the staged block's rows): wa holds, at lane l <
+// 32 = block row l, columns jw - 1 .. jw - 4 as bytes 0-3, wb columns jw - 5
+// .. jw - 8 (tb_win's upper 32 lanes moved down by one v_permlane32_swap), so
+// every step reads its record at lane r - base.  Per step, emit ALN | r at
+// lane j & 63; leave with st = 1, unmoved, when the cell's M tag is not a row
+// distance (a slot: the predecessor is 5+ rows back) or the predecessor lies
+// below the block, or, on the window's last column (j = 0 mod 8), when j
+// completes a 64-base chunk; else j -= 1, r -= the distance and, below the
+// last column, read the next record and leave with st = 2 when it is not
+// MPRED.  st = 0: moved past the last column (the caller swaps in the next
+// window).  The M tag is -d in 3-bit two's complement: s_bfe_i32 gives -d,
+// and li + (-d) carries exactly when the predecessor stays in the block (d <=
+// li) -- a slot tag (0..3) never carries -- so a step is 9 instructions, its
+// dependent chain s_bfe -> s_add -> v_readlane.  rec on entry: the current
+// cell's record (low byte); on exit the record of the cell (r, j) in the low
+// byte.  Hand-written: compiled, the multi-exit unrolled loop became a
+// flag-driven state machine of ~35 scalar instructions per step.
+__device__ __forceinline__ void tb_w8_steps(uint32_t k, uint32_t base, uint32_t wa, uint32_t wb, uint32_t &r,
                                             int32_t &j, uint32_t &rec, uint32_t &vev, uint32_t &st)
 {
     uint32_t t, li, c, jh, m0v;
     // the asm's scalar operands must live in SGPRs
     r = uni(r), j = uni(j), rec = uni(rec), k = uni(k), base = uni(base);
 // m0 = j & 63 is kept by the walk (the window's columns never cross a
-// 64-base chunk: jw = 0 mod 4 and the last column leaves on a completed
+// 64-base chunk: jw = 0 mod 8 and the last column leaves on a completed
 // chunk), j rebuilt from it at the exits
-#define TBW_M0 ""
-#define TBW_J "s_sub_u32 %[m0], %[m0], 1\n\t"
-#define TBW_ENTRY "s_and_b32 %[m0], %[j], 63\n\ts_andn2_b32 %[jh], %[j], 63\n\t"
-#define TBW_EXIT "s_or_b32 %[j], %[jh], %[m0]\n\t"
 #define TBW_HEAD(BFE, SLOW)                              \
-    TBW_M0                                               \
     "v_writelane_b32 %[vev], %[r], %[m0]\n\t"            \
-    "s_bfe_u32 %[t], %[rec], " BFE "\n\t"                \
-    TBW_LEAVE                       \
-    "s_cbranch_scc1 .Ltbw_" SLOW "%=\n\t"
+    "s_bfe_i32 %[t], %[rec], " BFE "\n\t"                \
+    "s_add_u32 %[li], %[li], %[t]\n\t"                   \
+    "s_cbranch_scc0 .Ltbw_" SLOW "%=\n\t"
 #define TBW_MOVE                                         \
-    TBW_J                                                \
-    "s_sub_u32 %[li], %[li], %[t]\n\t"                   \
-    "s_sub_u32 %[r], %[r], %[t]\n\t"
+    "s_sub_u32 %[m0], %[m0], 1\n\t"                      \
+    "s_add_u32 %[r], %[r], %[t]\n\t"
 #define TBW_NEXT(W, CODE, OUT)                           \
     "v_readlane_b32 %[rec], %[" W "], %[li]\n\t"         \
     "s_and_b32 %[c], %[rec], " CODE "\n\t"               \
     "s_cbranch_scc1 .Ltbw_" OUT "%=\n\t"
+#define TBW_BYTE(LBL, BFE, TO) \
+    ".Ltbw_" LBL "%=:\n\t"     \
+    "s_bfe_u32 %[rec], %[rec], " BFE "\n\t" \
+    "s_branch .Ltbw_" TO "%=\n"
     asm volatile(
-        "s_sub_u32 %[li], %[r], %[base]\n\t" TBW_ENTRY
+        "s_sub_u32 %[li], %[r], %[base]\n\t"
+        "s_and_b32 %[m0], %[j], 63\n\t"
+        "s_andn2_b32 %[jh], %[j], 63\n\t"
         "s_cmp_eq_u32 %[k], 0\n\t"
         "s_cbranch_scc1 .Ltbw_0%=\n\t"
-        "s_cmp_eq_u32 %[k], 2\n\t"
-        "s_cbranch_scc1 .Ltbw_2%=\n\t"
-        "s_lshl_b32 %[rec], %[rec], 16\n\t"  // k = 1 or 3: a high-half column
+        "s_cmp_gt_u32 %[k], 3\n\t"
+        "s_cbranch_scc1 .Ltbw_e4%=\n\t"
         "s_cmp_eq_u32 %[k], 1\n\t"
-        "s_cbranch_scc1 .Ltbw_1%=\n\t"
+        "s_cbranch_scc1 .Ltbw_e1%=\n\t"
+        "s_cmp_eq_u32 %[k], 2\n\t"
+        "s_cbranch_scc1 .Ltbw_e2%=\n\t"
+        "s_lshl_b32 %[rec], %[rec], 24\n\t"
         "s_branch .Ltbw_3%=\n"
-        ".Ltbw_0%=:\n\t" TBW_HEAD("0x60004", "slowlo") TBW_MOVE TBW_NEXT("wa", "0x30000", "outhi")
-        ".Ltbw_1%=:\n\t" TBW_HEAD("0x60014", "slowhi") TBW_MOVE TBW_NEXT("wb", "3", "outlo")
-        ".Ltbw_2%=:\n\t" TBW_HEAD("0x60004", "slowlo") TBW_MOVE TBW_NEXT("wb", "0x30000", "outhi")
-        ".Ltbw_3%=:\n\t" TBW_HEAD("0x60014", "slowhi")
+        ".Ltbw_e1%=:\n\t"
+        "s_lshl_b32 %[rec], %[rec], 8\n\t"
+        "s_branch .Ltbw_1%=\n"
+        ".Ltbw_e2%=:\n\t"
+        "s_lshl_b32 %[rec], %[rec], 16\n\t"
+        "s_branch .Ltbw_2%=\n"
+        ".Ltbw_e4%=:\n\t"
+        "s_cmp_eq_u32 %[k], 4\n\t"
+        "s_cbranch_scc1 .Ltbw_4%=\n\t"
+        "s_cmp_eq_u32 %[k], 5\n\t"
+        "s_cbranch_scc1 .Ltbw_e5%=\n\t"
+        "s_cmp_eq_u32 %[k], 6\n\t"
+        "s_cbranch_scc1 .Ltbw_e6%=\n\t"
+        "s_lshl_b32 %[rec], %[rec], 24\n\t"
+        "s_branch .Ltbw_7%=\n"
+        ".Ltbw_e5%=:\n\t"
+        "s_lshl_b32 %[rec], %[rec], 8\n\t"
+        "s_branch .Ltbw_5%=\n"
+        ".Ltbw_e6%=:\n\t"
+        "s_lshl_b32 %[rec], %[rec], 16\n\t"
+        "s_branch .Ltbw_6%=\n"
+        ".Ltbw_0%=:\n\t" TBW_HEAD("0x30004", "s0") TBW_MOVE TBW_NEXT("wa", "0x300", "o1")
+        ".Ltbw_1%=:\n\t" TBW_HEAD("0x3000c", "s1") TBW_MOVE TBW_NEXT("wa", "0x30000", "o2")
+        ".Ltbw_2%=:\n\t" TBW_HEAD("0x30014", "s2") TBW_MOVE TBW_NEXT("wa", "0x3000000", "o3")
+        ".Ltbw_3%=:\n\t" TBW_HEAD("0x3001c", "s3") TBW_MOVE TBW_NEXT("wb", "3", "o4")
+        ".Ltbw_4%=:\n\t" TBW_HEAD("0x30004", "s0") TBW_MOVE TBW_NEXT("wb", "0x300", "o1")
+        ".Ltbw_5%=:\n\t" TBW_HEAD("0x3000c", "s1") TBW_MOVE TBW_NEXT("wb", "0x30000", "o2")
+        ".Ltbw_6%=:\n\t" TBW_HEAD("0x30014", "s2") TBW_MOVE TBW_NEXT("wb", "0x3000000", "o3")
+        ".Ltbw_7%=:\n\t" TBW_HEAD("0x3001c", "s3")
         "s_cmp_eq_u32 %[m0], 0\n\t"
-        "s_cbranch_scc1 .Ltbw_slowhi%=\n\t" TBW_MOVE
+        "s_cbranch_scc1 .Ltbw_s3%=\n\t" TBW_MOVE
         "s_mov_b32 %[st], 0\n\t"
         "s_branch .Ltbw_clean%=\n"
-        ".Ltbw_slowhi%=:\n\t"
-        "s_lshr_b32 %[rec], %[rec], 16\n"
-        ".Ltbw_slowlo%=:\n\t"
+        // unmoved (st = 1): the current cell's byte
+        TBW_BYTE("s0", "0x80000", "slow")
+        TBW_BYTE("s1", "0x80008", "slow")
+        TBW_BYTE("s2", "0x80010", "slow")
+        TBW_BYTE("s3", "0x80018", "slow")
+        // a record that is not MPRED (st = 2): the new cell's byte
+        TBW_BYTE("o1", "0x80008", "out")
+        TBW_BYTE("o2", "0x80010", "out")
+        TBW_BYTE("o3", "0x80018", "out")
+        TBW_BYTE("o4", "0x80000", "out")
+        ".Ltbw_slow%=:\n\t"
         "s_mov_b32 %[st], 1\n\t"
         "s_branch .Ltbw_clean%=\n"
-        ".Ltbw_outhi%=:\n\t"
-        "s_lshr_b32 %[rec], %[rec], 16\n"
-        ".Ltbw_outlo%=:\n\t"
+        ".Ltbw_out%=:\n\t"
         "s_mov_b32 %[st], 2\n"
-        ".Ltbw_clean%=:\n\t" TBW_EXIT
-        "s_and_b32 %[rec], %[rec], 0xffff\n"
-        ".Ltbw_end%=:"
+        ".Ltbw_clean%=:\n\t"
+        "s_or_b32 %[j], %[jh], %[m0]\n"
         : [r] "+s"(r), [j] "+s"(j), [rec] "+s"(rec), [vev] "+v"(vev), [st] "=s"(st), [t] "=&s"(t), [li] "=&s"(li),
           [c] "=&s"(c), [jh] "=&s"(jh), [m0] "=&{m0}"(m0v)
         : [k] "s"(k), [base] "s"(base), [wa] "v"(wa), [wb] "v"(wb)
@@ -1966,10 +2062,7 @@ __device__ __forceinline__ void tb_w4_steps(uint32_t k, uint32_t base, uint32_t 
 #undef TBW_HEAD
 #undef TBW_MOVE
 #undef TBW_NEXT
-#undef TBW_M0
-#undef TBW_J
-#undef TBW_ENTRY
-#undef TBW_EXIT
+#undef TBW_BYTE
 }
 
 // the lower 32 lanes of wb <- the upper 32 lanes of the 64-lane window
@@ -1978,6 +2071,9 @@ __device__ __forceinline__ uint32_t tb_wb(uint32_t win)
     return (uint32_t)__builtin_amdgcn_permlane32_swap(win, win, false, false)[1];
 }
 
+// the M tag of a record: -d (d = 1..4 rows back) or a slot (0..3)
+__device__ __forceinline__ int32_t rec_mtag(uint32_t rec) { return (int32_t)(rec << 25) >> 29; }
+
 __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_t ej)
 {
     const uint32_t lane = lane_id();
@@ -1985,28 +2081,29 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     for (uint32_t j = ej + 1 + lane; j < m; j += 64) ev[j] = (EV_INS << 30) | er;
     uint32_t r = er, bi = er / kTbRows, buf = 0, base = bi * kTbRows;
     int32_t j = (int32_t)ej;
-    // per staged block, lane l < 32 = block row l: voff = its band offset,
-    // vrot = (tb_rot - 2 off) & 255, so cell (r, j) sits at byte
-    // ((buf * 32 + l) << 8) | ((vrot + 2 j) & 255) of the LDS; farm = the
-    // block's far rows (tags are slots)
+    // per staged block, lane l (mod 32) = block row l: voff = its band offset,
+    // vrot = (tb_rot - off) & 127, so cell (r, j) sits at byte
+    // ((buf * kTbRows + l) << 7) | ((vrot + j) & 127) of the LDS; farm = the
+    // block's far rows (their tags are in the far slot records)
     uint32_t voff = 0, vrot = 0, farm = 0;
     // record window of the plain MPRED steps: lane l holds the records of
-    // block row l & 31 at columns jw - 1 - 2 (l >> 5) (low half) and the
-    // column below it (high half), i.e. four columns of every staged row;
-    // valid while j lies in [jw - 4, jw) (entering a block invalidates it)
+    // block row l & 31 at columns jw - 1 - 4 (l >> 5) .. jw - 4 - 4 (l >> 5),
+    // i.e. eight columns of every staged row; valid while j lies in [jw - 8,
+    // jw) (entering a block invalidates it)
     uint32_t vrot32 = 0, rowb32 = 0, win = 0;
     int32_t jw = INT32_MIN / 2;
-    // the window below it (columns [jw - 8, jw - 4)), valid while jwn == jw
+    // the window below it (columns [jw - 16, jw - 8)), valid while jwn == jw
     uint32_t wnx = 0;
     int32_t jwn = INT32_MAX;
     auto enter = [&]() {
-        const uint32_t mt = (uint32_t)z.lds[kTbMeta + buf * 64 + lane];
+        const uint32_t l = lane & 31u;
+        const uint32_t mt = (uint32_t)z.lds[kTbMeta + buf * 32 + l];
         voff = mt & 0x7FFFFFFFu;
-        vrot = (tb_rot(base + lane) - 2u * voff) & 255u;  // (base: a multiple of kTbRows)
+        vrot = (tb_rot(base + l) - voff) & 127u;  // (base: a multiple of kTbRows)
         farm = (uint32_t)ballot((mt >> 31) != 0u) & (uint32_t)((1ull << kTbRows) - 1u);
-        // lanes 32-63 take lane l - 32's rotation (v_permlane32_swap: no LDS)
-        vrot32 = (uint32_t)__builtin_amdgcn_permlane32_swap(vrot, vrot, false, false)[0] - ((lane >> 5) * 4u);
-        rowb32 = (buf * kTbRows + (lane & (kTbRows - 1u))) << 8;
+        // lanes 32-63 hold the four columns below lanes 0-31's
+        vrot32 = vrot - (lane >> 5) * 4u;
+        rowb32 = (buf * kTbRows + (lane & (kTbRows - 1u))) << 7;
         jw = INT32_MIN / 2;
         jwn = INT32_MAX;
     };
@@ -2079,31 +2176,33 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         t_prev += ts1 - ts0;
 #endif
     };
-    // the record window of columns [jwv - 4, jwv) of the staged block (layout
-    // at vrot32 above); the compiler's lgkmcnt wait lands at the first use
+    // the record window of columns [jwv - 8, jwv) of the staged block (layout
+    // at vrot32 above: four byte reads per lane, a row's 128 B wrap); the
+    // compiler's lgkmcnt wait lands at the first use
     auto tb_win = [&](int32_t jwv) -> uint32_t {
-        const uint32_t a = vrot32 + 2u * (uint32_t)(jwv - 1);
-        const uint32_t lo = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | (a & 255u)));
-        const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds8 + (rowb32 | ((a - 2u) & 255u)));
-        return lo | hi << 16;
+        const uint32_t a = vrot32 + (uint32_t)(jwv - 1);
+        const uint32_t b0 = lds8[rowb32 | (a & 127u)];
+        const uint32_t b1 = lds8[rowb32 | ((a - 1u) & 127u)];
+        const uint32_t b2 = lds8[rowb32 | ((a - 2u) & 127u)];
+        const uint32_t b3 = lds8[rowb32 | ((a - 3u) & 127u)];
+        return b0 | b1 << 8 | b2 << 16 | b3 << 24;
     };
-    // the record of cell (r, j) from the current 4-column window, or the one
+    // the record of column jw - 1 - kk of row r from window w (kk < 8)
+    auto win_rec = [&](uint32_t w, uint32_t kk) -> uint32_t {
+        return ((uint32_t)__builtin_amdgcn_readlane((int)w, (int)((r - base) + ((kk & 4u) << 3))) >> ((kk & 3u) * 8u)) &
+               0xFFu;
+    };
+    // the record of cell (r, j) from the current 8-column window, or the one
     // below it, by one readlane; else the window holding column j is read
     // (one LDS round trip, which the window steps then reuse); r must lie in
     // the staged block
     auto rec_win = [&]() -> uint32_t {
         uint32_t kk = (uint32_t)(jw - 1 - j);
-        if (kk < 4u)
-            return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
-                    ((kk & 1u) * 16u)) & 0xFFFFu;
-        if (kk < 8u && jwn == jw)
-            return ((uint32_t)__builtin_amdgcn_readlane((int)wnx, (int)((r - base) + ((kk & 2u) << 4))) >>
-                    ((kk & 1u) * 16u)) & 0xFFFFu;
-        jw = (j & ~3) + 4;
+        if (kk < 8u) return win_rec(win, kk);
+        if (kk < 16u && jwn == jw) return win_rec(wnx, kk - 8u);
+        jw = (j & ~7) + 8;
         win = tb_win(jw);
-        kk = (uint32_t)(jw - 1 - j);
-        return ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((kk & 2u) << 4))) >>
-                ((kk & 1u) * 16u)) & 0xFFFFu;
+        return win_rec(win, (uint32_t)(jw - 1 - j));
     };
     auto cell = [&]() -> uint32_t {
         if (r < base) to_block();
@@ -2122,19 +2221,40 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         }
         --j;
     };
-    // to the predecessor given by the tag of cell (r, jc) (a slot on far
-    // rows; D: the D tag); far rows above 63 predecessors keep their slots in
-    // the wide records
-    auto to_pred = [&](uint32_t tag, int32_t jc, uint32_t isD) {
-        if ((farm >> (r - base)) & 1u) {
-            const uint32_t p0 = uni(poff[r]);
-            if (uni(poff[r + 1]) - p0 > 63u) {
-                const uint32_t t = (uint32_t)(jc - __builtin_amdgcn_readlane((int)voff, (int)(r - base)));
-                tag = uni((uint32_t)PX<const uint16_t>(z, kExtWtag)[(size_t)r * (kW * 2) + t * 2 + isD]);
+    // to the predecessor of cell (r, jc) given by its record rc8: the M tag
+    // (isD 0) or the D tag (1); an escape reads the distance from the row's
+    // tag plane (M on rings of up to 8 rows: 8 - tag); far rows keep their
+    // slots of the graph's predecessor list in a far slot record
+    auto to_pred = [&](uint32_t rc8, int32_t jc, uint32_t isD) {
+        const uint32_t li = r - base;
+        const bool far = (farm >> li) & 1u;
+        if (!isD) {
+            const int32_t mt = rec_mtag(rc8);
+            if (mt < 0 && !far) {
+                r = (uint32_t)((int32_t)r + mt);
+                return;
             }
-            r = uni(pred[p0 + tag]);
-        } else {
-            r -= tag;
+            if (kRing <= 8 && !far) {
+                r -= 8u - (uint32_t)mt;
+                return;
+            }
+        } else if ((rc8 & 0x80u) && !far) {
+            r -= 1u;
+            return;
+        }
+        const uint32_t t = (uint32_t)(jc - __builtin_amdgcn_readlane((int)voff, (int)li));
+        // the row's tag-plane row: staged in LDS (kTbTags) or in HBM
+        const uint8_t *tp = kTbTags ? lds8 + (kTbTag + buf * kTbBufWords) * 4 + li * kRecRow
+                                    : P<const uint8_t>(z, z.L.dsl) + (size_t)r * kRecRow;
+        if (far) {
+            const uint32_t p0 = uni(poff[r]);
+            const uint32_t fs = uni(*reinterpret_cast<const uint32_t *>(tp));
+            const uint32_t slot = uni((uint32_t)PX<const uint16_t>(z, kExtWtag)[(size_t)fs * (kW * 2) + t * 2 + isD]);
+            r = uni(pred[p0 + slot]);
+        } else if (kRing <= 8) {  // (D: 4 bits per cell)
+            r -= 1u + ((uni((uint32_t)tp[t >> 1]) >> ((t & 1u) * 4u)) & 15u);
+        } else {  // (a byte per cell: M | D << 4)
+            r -= 1u + ((uni((uint32_t)tp[t]) >> (isD * 4u)) & 15u);
         }
     };
     uint32_t rec = cell();
@@ -2149,22 +2269,22 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         const uint32_t hc = rec & 3u;
         bool emitted = false;  // (r, j) MPRED, emitted by the window steps: its move is pending
         if (hc == HC_MPRED && farm == 0u) {
-            // A block without far rows: plain steps through 4-column windows
-            // aligned to jw = 0 mod 4 (tb_w4_steps), the next window read
+            // A block without far rows: plain steps through 8-column windows
+            // aligned to jw = 0 mod 8 (tb_w8_steps), the next window read
             // from LDS while this one is walked.
             uint32_t k = (uint32_t)(jw - 1 - j);
-            if (k >= 4u) {
-                if (jwn == jw && k < 8u) {
+            if (k >= 8u) {
+                if (jwn == jw && k < 16u) {
                     win = wnx;  // j moved into the window below (already read)
-                    jw -= 4;
+                    jw -= 8;
                 } else {
-                    jw = (j & ~3) + 4;
+                    jw = (j & ~7) + 8;
                     win = tb_win(jw);
                 }
                 k = (uint32_t)(jw - 1 - j);
             }
             if (jwn != jw) {
-                wnx = tb_win(jw - 4);
+                wnx = tb_win(jw - 8);
                 jwn = jw;
             }
             uint32_t st;
@@ -2174,13 +2294,13 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
             z.pf[kPfRowA] += 1;
 #endif
             for (;;) {
-                tb_w4_steps(k, base, win, tb_wb(win), r, j, rec, vev, st);
+                tb_w8_steps(k, base, win, tb_wb(win), r, j, rec, vev, st);
                 if (st) break;
                 win = wnx;
-                jw -= 4;
-                wnx = tb_win(jw - 4);
+                jw -= 8;
+                wnx = tb_win(jw - 8);
                 jwn = jw;
-                rec = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(r - base)) & 0xFFFFu;
+                rec = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(r - base)) & 0xFFu;
                 if (rec & 3u) {
                     st = 2;
                     break;
@@ -2198,35 +2318,36 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
         if (hc == HC_MPRED) {  // state H
             if (!emitted) {
                 // plain steps while the next cell is in the block, the row not
-                // far, no chunk completes and no diagonal run starts
+                // far, no chunk completes and the M tag is a distance
                 for (;;) {
                     emit((EV_ALN << 30) | r);
-                    const uint32_t tag = (rec >> 4) & 63u;
+                    const int32_t mt = rec_mtag(rec);
                     const uint32_t li = r - base;
                     // sign-bit arithmetic keeps the test on the scalar unit (a
                     // compare of a bool lowers to VALU selects): far row, a chunk
-                    // completes ((j & 63) == 0), or the predecessor leaves the block
-                    const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | ((li - tag) >> 31)) & 1u;
+                    // completes ((j & 63) == 0), a slot tag, or the predecessor
+                    // leaves the block (li - d < 0)
+                    const uint32_t slow = ((farm >> li) | (((uint32_t)(j & 63) - 1u) >> 31) | (~(uint32_t)mt >> 31) |
+                                           ((li + (uint32_t)mt) >> 31)) & 1u;
                     if (slow) break;
                     --j;
-                    r -= tag;
-                    // r stays inside the block (tag < li): the next record comes
-                    // from the window by one readlane; an LDS round trip only
-                    // every fourth column
+                    r = (uint32_t)((int32_t)r + mt);
+                    // r stays inside the block: the next record comes from the
+                    // window by one readlane; an LDS round trip only every
+                    // eighth column
                     uint32_t k = (uint32_t)(jw - 1 - j);
-                    if (k >= 4u) {
-                        jw = (j & ~3) + 4;  // aligned, as the unrolled loop above assumes
+                    if (k >= 8u) {
+                        jw = (j & ~7) + 8;  // aligned, as the unrolled walk above assumes
                         win = tb_win(jw);
                         k = (uint32_t)(jw - 1 - j);
                     }
-                    rec = ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)((r - base) + ((k & 2u) << 4))) >>
-                           ((k & 1u) * 16u)) & 0xFFFFu;
+                    rec = win_rec(win, k);
                     if ((rec & 3u) != HC_MPRED) break;
                 }
                 if ((rec & 3u) != HC_MPRED) continue;
             }
             step_j();
-            to_pred((rec >> 4) & 63u, j + 1, 0u);  // the MPRED cell is (r, j + 1)
+            to_pred(rec, j + 1, 0u);  // the MPRED cell is (r, j + 1)
             if (r < base) to_block();
             rec = rec_win();
             DP_STAMP(kPfTbStep);
@@ -2251,7 +2372,7 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 z.pf[kPfTbDsteps] += 1;
 #endif
                 const uint32_t ext = rec & 4u;
-                to_pred((rec >> 10) & 63u, j, 1u);
+                to_pred(rec, j, 1u);
                 if (r < base) to_block();
                 rec = rec_win();
                 if (!ext || ++guard > glim) break;
@@ -2603,8 +2724,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
     }
     // predecessor lists of the new graph, and each row's DP record
     // {base | chain << 3 | np << 8, p0, p1, p2} + p3 (dp_fast's prefetch)
-    uint4 *rrec = P<uint4>(z, z.L.rrec);
-    uint32_t *rp3 = P<uint32_t>(z, z.L.rp3);
+    uint2 *rrec = P<uint2>(z, z.L.rrec);
     // (PB rows per thread per pass, loads first)
 #ifndef CCSX_MERGE_PB
 #define CCSX_MERGE_PB 2
@@ -2664,16 +2784,11 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
         }
         const uint32_t chain = (np == 1 && ps[0] + 1 == n) ? kInfoChain : 0u;
         const uint32_t info = (nb[x] & 3u) | chain | far | (np << 8);
-        if constexpr (kHelpers == 0) {
-            // {info, the predecessors' row distances} (RowPre::dpk; only read on rows without the far flag)
-            uint32_t dpk = 0;
+        // {info, the predecessors' tag bytes} (RowPre::dpk; only read on rows without the far flag)
+        uint32_t dpk = 0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) dpk |= ((uint32_t)u < np ? (n - ps[u]) & 255u : 0u) << (8 * u);
-            *reinterpret_cast<uint2 *>(rrec + n) = make_uint2(info, dpk);
-        } else {
-            rrec[n] = make_uint4(info, ps[0], ps[1], ps[2]);
-            rp3[n] = ps[3];
-        }
+        for (int u = 0; u < 4; ++u) dpk |= ((uint32_t)u < np ? tagb(n - ps[u]) & 255u : 0u) << (8 * u);
+        rrec[n] = make_uint2(info, dpk);
       }
     }
     for (uint32_t i = tid; i < K; i += T) {
@@ -2685,12 +2800,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
             if (n - ad > (uint32_t)kRing) spf[ad] = 1;
             info |= (1u << 8) | (ad + 1 == n ? kInfoChain : 0u) | (n - ad > (uint32_t)kRing ? kInfoFar : 0u);
         }
-        if constexpr (kHelpers == 0) {
-            *reinterpret_cast<uint2 *>(rrec + n) = make_uint2(info, ad != kNone ? (n - ad) & 255u : 0u);
-        } else {
-            rrec[n] = make_uint4(info, ad != kNone ? ad : 0u, 0u, 0u);
-            rp3[n] = 0;
-        }
+        rrec[n] = make_uint2(info, ad != kNone ? tagb(n - ad) & 255u : 0u);
     }
         DP_STAMP(kPfRowE);
     // M5: first/last rows of the reads

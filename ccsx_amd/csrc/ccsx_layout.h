@@ -18,6 +18,7 @@
 namespace ccsx {
 
 constexpr int kW = 128;        // DP band (main.c:849 bandwidth = 128)
+constexpr uint32_t kRecRow = kW;  // bytes of a DP row's cell records (8 bits per cell)
 // DP rows back whose H / D a row reads from the LDS ring (farther
 // predecessors: HBM spill records); per kernel configuration
 #ifndef CCSX_RING
@@ -93,7 +94,7 @@ struct ZmwDesc {
     uint32_t seg0;      // index of the first segment in the segment arrays
     uint32_t n;         // number of segments (pushed reads)
     uint32_t rcap, ecap, lcap, scap, nw;
-    uint32_t wcap;      // rows of wide slot records (rcap if n > 64, else 0)
+    uint32_t wcap;      // far-row slot records (rows flagged far: u16 M / D slots per cell)
     uint32_t outcap;    // output slab capacity (bytes)
     uint32_t msacap;    // MSA slab capacity (bytes)
     uint64_t bp_off;    // breakpoint log (-v >= 3): word offset of {rounds, (i, ncols) x bpcap}
@@ -103,7 +104,7 @@ struct ZmwDesc {
 
 struct ZLayout {
     uint64_t nb0, mem0, poff0, pred0, nb1, mem1, poff1, pred1;
-    uint64_t rmeta, spf, sslot, codes, spill, rrec, rp3;
+    uint64_t rmeta, spf, sslot, codes, dsl, spill, rrec;
     uint64_t ev, tgt, ipt, iinf, ifix, cnt, fixf, addp, cntn;
     uint64_t colof, cons, cmask, colrow, rdoff, rdlen, rfirst, rlast, rfc, rlc;
     uint64_t ext;  // rarely used regions (zext): kept as one offset to spare registers
@@ -113,10 +114,10 @@ struct ZLayout {
 CCSX_HD inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
 // The extension regions, in order (offsets relative to ZLayout::ext):
-//  * ZMWs of more than 64 segments (whose far rows can have more than 63
-//    predecessors, more than a 6-bit slot tag holds): a wide slot record per
-//    row (per cell the M and D predecessor slots, u16 each: 512 B per row),
-//    written for rows above 63 predecessors only;
+//  * the far rows' slot records (rows with more than four predecessors or one
+//    beyond the DP ring, whose 8-bit cell records carry no tags): per cell the
+//    M and D predecessor slots, u16 each, 512 B per far row, taken in the
+//    order the DP meets them (the row's index in its tag-plane row, word 0);
 //  * the HBM-read kernel instance (reads beyond the LDS read buffer): the read
 //    as 2-bit codes and the shredding cursors.
 enum ZExt { kExtWtag = 0, kExtRdbuf, kExtPos, kExtEnd };
@@ -157,10 +158,10 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
     L.rmeta = take(uint64_t(d.rcap) * 4);              // per DP row: band offset | far flag << 31
     L.spf = take(d.rcap);                              // per row: needed beyond the LDS ring
     L.sslot = take(uint64_t(d.rcap) * 4);              // per spilled row: its spill record
-    L.codes = take(uint64_t(d.rcap) * 256);            // cell records, 16 bits/cell, 256 B/row
+    L.codes = take(uint64_t(d.rcap) * kRecRow);        // cell records, 8 bits/cell, 128 B/row
+    L.dsl = take(uint64_t(d.rcap) * kRecRow);          // per row: tag plane, escape distances (far rows: word 0 = far record)
     L.spill = take(uint64_t(d.scap) * (kW * 8 + 16));  // spilled rows: H, D, band offset, row-max key
-    L.rrec = take(uint64_t(d.rcap) * 16);              // per row: {info, p0, p1, p2} for the DP prefetch
-    L.rp3 = take(uint64_t(d.rcap) * 4);                // per row: 4th predecessor
+    L.rrec = take(uint64_t(d.rcap) * 8);               // per row: {info, the predecessors' tag bytes} for the DP prefetch
     L.ev = take(uint64_t(d.lcap) * 4);
     L.tgt = take(uint64_t(d.lcap) * 4);
     L.ipt = take(uint64_t(d.lcap) * 4);
@@ -220,9 +221,10 @@ CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, boo
     }
     d.lcap = lmax + 16;
     d.nw = (n + 63) / 64 ? (n + 63) / 64 : 1;
-    // in-degree <= reads pushed before (one in-edge per target per read), so
-    // only ZMWs of >= 65 segments can have rows above 63 predecessors
-    d.wcap = n > 64 ? d.rcap : 0;
+    // far rows' slot records: every row (full caps), else 1 in 16 (config E
+    // 0.02 %, D 0.87 % of DP rows are far); more fail the ZMW with kErrSpill
+    // and it is re-run with full caps
+    d.wcap = full ? d.rcap : d.rcap / 16 + 64;
     d.outcap = uint32_t(S + 16);
     if (!full) {
         const uint64_t oc = tight_out ? tight_out : 2ull * lmax + 1024;

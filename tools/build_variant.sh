@@ -4,13 +4,15 @@
 # (after its own defines, so they override them) and to the host launcher;
 # the configurations' defines come from ccsx_amd/build.py (KCFGS).
 #   [CFGS="tput occ"] [KSRC=path/to/kernel.hip] [KSCHED="..."] tools/build_variant.sh TAG -DFOO=1 ...
+# CSRC=dir takes ccsx_kernel.hip, ccsx_gpu.cpp and their headers from dir.
 # CFGS limits the variant to the named configurations (default: all): the
 # others reuse the product's objects (also when KSRC names another source).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TAG=$1; shift
 OBJ=$ROOT/build/obj
-C=$ROOT/ccsx_amd/csrc
+# CSRC: another source tree (e.g. a git archive of an older commit) for the kernel and ccsx_gpu.cpp
+C=${CSRC:-$ROOT/ccsx_amd/csrc}
 INC="-I$ROOT/include -I$C -I$C/host"
 # KSCHED overrides the machine-scheduler flags (default: build.py's max-ilp; KSCHED=" " for LLVM's default)
 K="/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC ${KSCHED:--mllvm -amdgpu-sched-strategy=max-ilp} -Wno-macro-redefined"
