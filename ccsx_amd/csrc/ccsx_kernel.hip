@@ -1143,6 +1143,12 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
     }
 }
 
+// the DP's cell records and, after them, its tag plane (row_slots)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const Z &z)
+{
+    return brsrc(z.ws + z.L.codes, (uint32_t)(z.L.dsl - z.L.codes) + z.R * kRecRow);
+}
+
 // The records beside a row's cell bytes: a far row's slot record (u16 M / D
 // slot per cell, its index in word 0 of the row's tag-plane row), or, for a
 // row with a predecessor more than one row back, its tag plane: the D
@@ -1151,8 +1157,13 @@ __device__ __forceinline__ void dpB_cold(Z &z, const BState &S, uint32_t r, uint
 // (Buffer stores: a store through a generic pointer is a flat store, which
 // also counts in lgkmcnt, so the next row's wait on its ring reads would wait
 // for it to reach memory.)
-__device__ __forceinline__ void row_slots(Z &z, uint32_t r, uint32_t info, const PredAcc &A)
+__device__ __forceinline__ void row_slots(Z &z, const __amdgpu_buffer_rsrc_t &rc, uint32_t r, uint32_t info,
+                                          const PredAcc &A)
 {
+    // the tag plane follows the records: the records' descriptor (rec_rsrc)
+    // reaches it at this scalar offset (a descriptor of its own cost the
+    // helpers ~10 SGPR spill reloads per row, config B +4 %)
+    const uint32_t tpo = (uint32_t)(z.L.dsl - z.L.codes);
     const uint32_t lane = lane_id();
     if (info & kInfoFar) {
         const uint32_t fs = z.nfar;
@@ -1162,20 +1173,18 @@ __device__ __forceinline__ void row_slots(Z &z, uint32_t r, uint32_t info, const
             const auto fr = brsrc(PX<uint8_t>(z, kExtWtag), z.d.wcap * (kW * 4u));
             __builtin_amdgcn_raw_buffer_store_b64(v2u{A.ms0 | (A.ds0 << 16), A.ms1 | (A.ds1 << 16)}, fr,
                                                   fs * (kW * 4u) + lane * 8u, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(fs, brsrc(P<uint8_t>(z, z.L.dsl), z.R * kRecRow),
-                                                  lane == 0 ? r * kRecRow : ~0u, 0, 0);
+            if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(fs, rc, r * kRecRow, tpo, 0);
         } else {
             z.status = kErrSpill;  // (re-run with full caps: a far slot record per row)
         }
     } else if (!(info & kInfoChain)) {
-        const auto tpr = brsrc(P<uint8_t>(z, z.L.dsl), z.R * kRecRow);
         if constexpr (kRing <= 8) {
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((A.ds0 & 15u) | ((A.ds1 & 15u) << 4)), tpr, r * kRecRow + lane, 0,
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((A.ds0 & 15u) | ((A.ds1 & 15u) << 4)), rc, r * kRecRow + lane, tpo,
                                                  0);
         } else {
             __builtin_amdgcn_raw_buffer_store_b16(
-                (unsigned short)((A.ms0 & 15u) | ((A.ds0 & 15u) << 4) | ((A.ms1 & 15u) << 8) | ((A.ds1 & 15u) << 12)), tpr,
-                r * kRecRow + lane * 2u, 0, 0);
+                (unsigned short)((A.ms0 & 15u) | ((A.ds0 & 15u) << 4) | ((A.ms1 & 15u) << 8) | ((A.ds1 & 15u) << 12)), rc,
+                r * kRecRow + lane * 2u, tpo, 0);
         }
     }
 }
@@ -1215,7 +1224,7 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
     uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 & 0x70u) | (A.ds0 & 0x80u);
     uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 & 0x70u) | (A.ds1 & 0x80u);
-    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, r, info, A);
+    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, rc, r, info, A);
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
     // H' at j = m - 1
     const int32_t eb = (off << 1) + x.em1;
@@ -1273,7 +1282,7 @@ __device__ __forceinline__ void row_record_solo(Z &z, int32_t &bE, uint32_t &bKe
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
     uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 & 0x70u) | (A.ds0 & 0x80u);
     uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 & 0x70u) | (A.ds1 & 0x80u);
-    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, r, info, A);
+    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, rc, r, info, A);
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1 = X + eb
     // (x.em1 carries -kXBias), and H' at j = m - 1 (+3)
     const int32_t eb = (off << 1) + x.em1;
@@ -1478,7 +1487,7 @@ __device__ __forceinline__ void dp_wave_b(Z &z, uint32_t m, uint32_t h)
     S.wc0 = 0, S.wnc = 2;
     S.W.cur = RowPre{0, 0};
     S.W.nxt = S.W.cur;
-    S.rc = brsrc(z.ws + z.L.codes, z.R * kRecRow);
+    S.rc = rec_rsrc(z);
     z.nfar = h;
     const uint32_t nblk = dp_nblk(z.R);
 #ifdef CCSX_DP_STAMPS
@@ -1747,7 +1756,7 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     S.W.nxt = S.W.cur;
     SolB B;
     B.bE = INT32_MIN, B.bKey = 0;
-    B.rc = brsrc(z.ws + z.L.codes, z.R * kRecRow);
+    B.rc = rec_rsrc(z);
     z.nfar = 0;
     const uint32_t nblk = dp_nblk(z.R);
     for (uint32_t b = 0; b < nblk && !z.status; ++b) {
