@@ -440,11 +440,14 @@ __device__ __forceinline__ uint32_t win_codes(uint32_t win, int32_t off, int32_t
 
 // The 8-bit cell record (row_record): code (bits 0-1) | D-ext (2) | I-ext (3)
 // | M tag (4-6) | D tag (7).  M tag: -d as 3-bit two's complement for the
-// predecessor d = 1..4 rows back, else (0..3) an escape; D tag: 1 = row r - 1,
-// else an escape.  An escape's distance d - 1 sits in the row's tag plane (D:
-// 4 bits per cell; M too where the ring is longer than 8 rows -- on the
-// others an M escape is (-d) & 7 = 8 - d for d = 5..8).  Rows flagged far
-// carry neither: their slots go to a far slot record.  The tag byte of a
+// predecessor d = 1..4 rows back, else (0..3) an escape.  Rows of one or two
+// predecessors (not far) carry their distances in the row meta (rmeta_word):
+// the D tag is the predecessor's slot, an M escape's low bit too.  Rows of 3-4
+// predecessors: D tag 1 = row r - 1, else an escape; an escape's distance
+// d - 1 sits in the row's tag plane (D: 4 bits per cell; M too where the ring
+// is longer than 8 rows -- on the others an M escape is (-d) & 7 = 8 - d for
+// d = 5..8).  Rows flagged far carry neither: their slots go to a far slot
+// record.  The tag byte of a
 // predecessor d rows back (what pred_fold keeps per cell; d <= kRing on rows
 // not flagged far): M tag << 4 | D tag << 7 | (d - 1).  merge computes them
 // into the DP's row records (RowPre::dpk): in the DP the arithmetic took ~9
@@ -456,7 +459,13 @@ __device__ __forceinline__ uint32_t tagb(uint32_t d)
     // d = 8, 1, 2, 3 | 4, 5, 6, 7 by d & 3; beyond 8 rows: M escape 0, D escape
     return d > 8u ? d - 1u : ((d & 4u) ? 0x16253443u : 0x5261F007u) >> ((d & 3u) * 8u);
 }
-constexpr uint32_t kTagPrev = 0xF0u;  // tagb(1): the previous row
+// a row of one or two predecessors: the D tag (and an M escape's low bit) is the slot
+__device__ __forceinline__ uint32_t tagb2(uint32_t d, uint32_t s)
+{
+    const uint32_t t = tagb(d) & 0x7Fu;
+    return (t & 0x70u) < 0x40u ? (t & 0x0Fu) | (s << 7) | (s << 4) : t | (s << 7);
+}
+constexpr uint32_t kTagPrev = 0x70u;  // tagb2(1, 0): the previous row, slot 0
 static_assert(kRing <= 16, "tag bytes hold distances up to 16");
 
 // per lane: row r0+lane's info and the tag bytes of its first four
@@ -482,6 +491,17 @@ __device__ __forceinline__ uint32_t row_pred(const RowPre &W, uint32_t r, int li
 {
     return r - 1u - (row_tag(W, li, k) & 15u);
 }
+
+// the row meta word the traceback stages with each record block: band offset
+// (< 2^22) | for a row of one or two predecessors (not far) the distances - 1
+// of slots 0 / 1 << 22 / 26 and bit 30 | far << 31
+__device__ __forceinline__ uint32_t rmeta_word(uint32_t off, uint32_t info, uint32_t dpk)
+{
+    const bool far = (info & kInfoFar) != 0u;
+    const bool two = !far && (info >> 8) <= 2u;
+    return off | (far ? 0x80000000u : 0u) | (two ? 0x40000000u | ((dpk & 15u) << 22) | (((dpk >> 8) & 15u) << 26) : 0u);
+}
+constexpr uint32_t kMetaOff = 0x3FFFFFu;
 
 // the DP's row records {info, tag bytes} (written by merge): coalesced, no
 // dependent loads
@@ -1151,9 +1171,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const Z &z)
 
 // The records beside a row's cell bytes: a far row's slot record (u16 M / D
 // slot per cell, its index in word 0 of the row's tag-plane row), or, for a
-// row with a predecessor more than one row back, its tag plane: the D
-// distance - 1 per cell, 4 bits (and the M one beside it, a byte per cell,
-// where the ring is longer than 8 rows).  A chain row needs neither.
+// row of 3-4 predecessors, its tag plane: the D distance - 1 per cell, 4 bits
+// (and the M one beside it, a byte per cell, where the ring is longer than 8
+// rows).  Rows of one or two predecessors need neither (rmeta_word).
 // (Buffer stores: a store through a generic pointer is a flat store, which
 // also counts in lgkmcnt, so the next row's wait on its ring reads would wait
 // for it to reach memory.)
@@ -1177,7 +1197,7 @@ __device__ __forceinline__ void row_slots(Z &z, const __amdgpu_buffer_rsrc_t &rc
         } else {
             z.status = kErrSpill;  // (re-run with full caps: a far slot record per row)
         }
-    } else if (!(info & kInfoChain)) {
+    } else {
         if constexpr (kRing <= 8) {
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((A.ds0 & 15u) | ((A.ds1 & 15u) << 4)), rc, r * kRecRow + lane, tpo,
                                                  0);
@@ -1224,7 +1244,7 @@ __device__ __forceinline__ void row_record(Z &z, int32_t &bE, uint32_t &bKey, in
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
     uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 & 0x70u) | (A.ds0 & 0x80u);
     uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 & 0x70u) | (A.ds1 & 0x80u);
-    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, rc, r, info, A);
+    if (cold && ((info & kInfoFar) || (info >> 8) >= 3u)) row_slots(z, rc, r, info, A);
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1, and
     // H' at j = m - 1
     const int32_t eb = (off << 1) + x.em1;
@@ -1282,7 +1302,7 @@ __device__ __forceinline__ void row_record_solo(Z &z, int32_t &bE, uint32_t &bKe
     const uint32_t hc1 = i1 ? HC_INS : d1 ? HC_DEL : mp1 ? HC_MPRED : HC_MSRC;
     uint32_t w0 = hc0 | A.dx0 | iext0 | (A.ms0 & 0x70u) | (A.ds0 & 0x80u);
     uint32_t w1 = hc1 | A.dx1 | iext1 | (A.ms1 & 0x70u) | (A.ds1 & 0x80u);
-    if (cold && (info & (kInfoChain | kInfoFar)) != kInfoChain) row_slots(z, rc, r, info, A);
+    if (cold && ((info & kInfoFar) || (info >> 8) >= 3u)) row_slots(z, rc, r, info, A);
     // free-end candidates (SPEC.md §3.5) on H': e = H' + 2j - 2m - 1 = X + eb
     // (x.em1 carries -kXBias), and H' at j = m - 1 (+3)
     const int32_t eb = (off << 1) + x.em1;
@@ -1402,9 +1422,9 @@ __device__ __forceinline__ void dpB_block(Z &z, BState &S, uint32_t r0, uint32_t
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
     if (h == 0 && ((r0 & 15u) == 16u - kBlkAB || rend == R)) {
         const uint32_t g0 = r0 & ~15u;
-        const uint32_t far = (S.W.cur.info & kInfoFar) ? 0x80000000u : 0u;
         const auto rm = brsrc(reinterpret_cast<uint32_t *>(z.ws + z.L.rmeta) + g0, (rend - g0) * 4);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vOff | far, rm, (uint32_t)(lane - (int)(g0 & 63u)) * 4u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(rmeta_word((uint32_t)vOff, S.W.cur.info, S.W.cur.dpk), rm,
+                                              (uint32_t)(lane - (int)(g0 & 63u)) * 4u, 0, 0);
     }
     recwin_end(S.W, r0);
 }
@@ -1726,9 +1746,9 @@ __device__ __forceinline__ void dpS_block(Z &z, AState &S, SolB &B, uint32_t r0,
     const uint32_t rend = r0 + kBlkAB < R ? r0 + kBlkAB : R;
     if ((r0 & 15u) == 16u - kBlkAB || rend == R) {
         const uint32_t g0 = r0 & ~15u;
-        const uint32_t far = (S.W.cur.info & kInfoFar) ? 0x80000000u : 0u;
         const auto rm = brsrc(reinterpret_cast<uint32_t *>(z.ws + z.L.rmeta) + g0, (rend - g0) * 4);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)S.vOff | far, rm, (uint32_t)(lane - (int)(g0 & 63u)) * 4u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(rmeta_word((uint32_t)S.vOff, S.W.cur.info, S.W.cur.dpk), rm,
+                                              (uint32_t)(lane - (int)(g0 & 63u)) * 4u, 0, 0);
     }
     recwin_end(S.W, r0);
 }
@@ -1781,7 +1801,7 @@ __device__ __forceinline__ void dp_solo(Z &z, uint32_t m, uint32_t &er_out, uint
     int32_t boff = 0;
     if (best != INT32_MIN) {
         const auto rm = brsrc(reinterpret_cast<uint32_t *>(z.ws + z.L.rmeta), z.R * 4u);
-        boff = (int32_t)(uni(__builtin_amdgcn_raw_buffer_load_b32(rm, (uint32_t)rmin * 4u, 0, 1)) & 0x7FFFFFFFu);
+        boff = (int32_t)(uni(__builtin_amdgcn_raw_buffer_load_b32(rm, (uint32_t)rmin * 4u, 0, 1)) & kMetaOff);
     }
     const int32_t jsel = mine ? boff + 2 * lane + (int32_t)(B.bKey & 1u) : INT32_MAX;
     er_out = best == INT32_MIN ? 0xFFFFFFFFu : (uint32_t)rmin;
@@ -2107,8 +2127,8 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
     auto enter = [&]() {
         const uint32_t l = lane & 31u;
         const uint32_t mt = (uint32_t)z.lds[kTbMeta + buf * 32 + l];
-        voff = mt & 0x7FFFFFFFu;
-        vrot = (tb_rot(base + l) - voff) & 127u;  // (base: a multiple of kTbRows)
+        voff = mt;  // (the whole meta word: its band offset is voff & kMetaOff)
+        vrot = (tb_rot(base + l) - (mt & kMetaOff)) & 127u;  // (base: a multiple of kTbRows)
         farm = (uint32_t)ballot((mt >> 31) != 0u) & (uint32_t)((1ull << kTbRows) - 1u);
         // lanes 32-63 hold the four columns below lanes 0-31's
         vrot32 = vrot - (lane >> 5) * 4u;
@@ -2243,15 +2263,24 @@ __device__ __forceinline__ void traceback(Z &z, uint32_t m, uint32_t er, uint32_
                 r = (uint32_t)((int32_t)r + mt);
                 return;
             }
+        }
+        const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)voff, (int)li);
+        if (!far && (meta & 0x40000000u)) {
+            // one or two predecessors: the tag names the slot, the row meta its distance
+            const uint32_t slot = isD ? (rc8 >> 7) & 1u : (rc8 >> 4) & 1u;
+            r -= 1u + ((meta >> (22u + 4u * slot)) & 15u);
+            return;
+        }
+        if (!isD) {
             if (kRing <= 8 && !far) {
-                r -= 8u - (uint32_t)mt;
+                r -= 8u - (uint32_t)rec_mtag(rc8);
                 return;
             }
         } else if ((rc8 & 0x80u) && !far) {
             r -= 1u;
             return;
         }
-        const uint32_t t = (uint32_t)(jc - __builtin_amdgcn_readlane((int)voff, (int)li));
+        const uint32_t t = (uint32_t)(jc - (int32_t)(meta & kMetaOff));
         // the row's tag-plane row: staged in LDS (kTbTags) or in HBM
         const uint8_t *tp = kTbTags ? lds8 + (kTbTag + buf * kTbBufWords) * 4 + li * kRecRow
                                     : P<const uint8_t>(z, z.L.dsl) + (size_t)r * kRecRow;
@@ -2794,9 +2823,11 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
         const uint32_t chain = (np == 1 && ps[0] + 1 == n) ? kInfoChain : 0u;
         const uint32_t info = (nb[x] & 3u) | chain | far | (np << 8);
         // {info, the predecessors' tag bytes} (RowPre::dpk; only read on rows without the far flag)
+        const bool two = np <= 2u && !far;
         uint32_t dpk = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) dpk |= ((uint32_t)u < np ? tagb(n - ps[u]) & 255u : 0u) << (8 * u);
+        for (int u = 0; u < 4; ++u)
+            dpk |= ((uint32_t)u < np ? (two ? tagb2(n - ps[u], (uint32_t)u) : tagb(n - ps[u])) & 255u : 0u) << (8 * u);
         rrec[n] = make_uint2(info, dpk);
       }
     }
@@ -2809,7 +2840,7 @@ __device__ __forceinline__ void merge(Z &z, uint32_t k, uint32_t m, uint32_t tid
             if (n - ad > (uint32_t)kRing) spf[ad] = 1;
             info |= (1u << 8) | (ad + 1 == n ? kInfoChain : 0u) | (n - ad > (uint32_t)kRing ? kInfoFar : 0u);
         }
-        rrec[n] = make_uint2(info, ad != kNone ? tagb(n - ad) & 255u : 0u);
+        rrec[n] = make_uint2(info, ad != kNone ? tagb2(n - ad, 0u) & 255u : 0u);
     }
         DP_STAMP(kPfRowE);
     // M5: first/last rows of the reads
