@@ -368,8 +368,10 @@ constexpr uint32_t kLdsReadMaxBases = 100000, kLdsMaxSegs = 4096;
 // slices of at least this many times the occupancy configuration's resident
 // workgroups run the solo configuration
 constexpr size_t kSoloSliceFactor = 3;
-// segments per ZMW (slice mean) below which a solo16 slice runs solo16w
-constexpr uint32_t kSolo16WMaxSegs = 16;
+// segments per ZMW (slice mean) below which a solo16 slice runs solo16w (24
+// ZMWs per CU, 80 VGPRs); 16 until the 8-bit records, with which solo16w also
+// runs config D's 30-segment ZMWs 2.2 % faster (305.9 vs 312.7 ms, r06w)
+constexpr uint32_t kSolo16WMaxSegs = 64;
 
 // launch classes of ccsx_gpu_run's slices: LDS read buffer up to 32 kb (4+
 // workgroups per CU), up to kLdsReadMaxBases, HBM-read instance; slices never

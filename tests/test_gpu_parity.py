@@ -392,8 +392,12 @@ def test_large_slice_picks_solo(engine):
     engine.set_kernel_cfg(-1)
     _check(engine, zs, cx.MODE_SHRED, threads=16)
     assert engine.kernel_cfg() == 5  # solo16w: a tight-cap shredded slice of 6-segment ZMWs on the LDS instance
-    # ZMWs of 20 segments take solo16 (20 per CU, 96 VGPRs)
+    # ZMWs of 20 segments too (config D's shape: solo16w since the 8-bit records)
     zs = [synth(81000 + h, 300, 20) for h in range(4096)]
+    _check(engine, zs, cx.MODE_SHRED, threads=16)
+    assert engine.kernel_cfg() == 5
+    # ZMWs of 66 segments take solo16 (20 per CU, 96 VGPRs)
+    zs = [synth(82000 + h, 150, 66) for h in range(4096)]
     _check(engine, zs, cx.MODE_SHRED, threads=16)
     assert engine.kernel_cfg() == 4
 
