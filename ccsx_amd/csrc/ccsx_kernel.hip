@@ -1917,11 +1917,16 @@ constexpr uint32_t kTbBufs = CCSX_TB_BUFS;
 #else
 constexpr uint32_t kTbBufs = (uint32_t)kRingWords >= 2 * (kTbBufWords + 32) ? 2u : 1u;
 #endif
-// the blocks' tag-plane rows staged beside them where the area holds both (the
-// latency objects, whose single ZMW per SIMD would otherwise wait ~2 us on
-// HBM for each escape on its serial walk; the one-wave objects' other ZMWs
-// cover those waits)
-constexpr bool kTbTags = (uint32_t)kRingWords >= kTbBufs * (2 * kTbBufWords + 32);
+// CCSX_TB_TAGS=1: the blocks' tag-plane rows staged beside them where the area
+// holds both (measurement variant: it saved the latency objects' serial walk
+// ~2 us of HBM per escape while every row with a predecessor more than one row
+// back escaped through the plane; since rows of one or two predecessors carry
+// their distances in the row meta, the extra DMA costs config B 0.7 %, r06z)
+#ifdef CCSX_TB_TAGS
+constexpr bool kTbTags = CCSX_TB_TAGS && (uint32_t)kRingWords >= kTbBufs * (2 * kTbBufWords + 32);
+#else
+constexpr bool kTbTags = false;
+#endif
 constexpr uint32_t kTbTag = kTbBufs * kTbBufWords;  // LDS word of the staged tag-plane rows (kTbTags)
 constexpr uint32_t kTbMeta = (kTbTags ? 2 : 1) * kTbBufs * kTbBufWords;  // LDS word of the row meta (32 words per buffer)
 static_assert(kTbMeta + kTbBufs * 32 <= (uint32_t)kRingWords, "traceback buffers live in the DP ring area");
