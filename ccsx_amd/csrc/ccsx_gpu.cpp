@@ -235,6 +235,7 @@ struct ccsx_ctx {
     bool profiling = false;
     uint32_t tight_rows = 0;           // test hook: override the tight row cap
     uint32_t tight_out = 0;            // test hook: override the tight output slab
+    uint32_t tight_far = 0;            // test hook: override the tight far slot record rows
     uint64_t stage_piece = 0;          // test hook: piecewise staging's half size (0: kStagePiece)
     int64_t fault = -1;                // test hook: report this ZMW of the next run as failed
     bool shred_caps = false;           // tight caps sized for shredding windows (ccsx_gpu_run, shredded mode)
@@ -406,7 +407,7 @@ static uint64_t zmw_bytes(const ccsx_zmw_in &zi, bool full, const ccsx_ctx *c, u
     uint32_t lmax;
     zmw_extent(zi, S, hi, lmax);
     ccsx::ZmwDesc d{};
-    ccsx::zcaps(d, S, lmax, zi.nseg, full, c->tight_rows, shred_win, c->tight_out);
+    ccsx::zcaps(d, S, lmax, zi.nseg, full, c->tight_rows, shred_win, c->tight_out, c->tight_far);
     ccsx::ZLayout L;
     ccsx::zlayout(L, d);
     return ccsx::align256(L.total) + hi + d.outcap + uint64_t(zi.nseg) * 8 + sizeof(ccsx::ZmwDesc) + 32;
@@ -474,7 +475,7 @@ static int stage_slot(ccsx_ctx *c, Slot &s, const ccsx_zmw_in *z, size_t nz, int
         }
         ccsx::ZmwDesc &d = s.desc[i];
         ccsx::zcaps(d, S, lmax, zi.nseg, full_caps != 0, c->tight_rows, c->shred_caps ? c->shred_read_cap : 0u,
-                    c->tight_out);
+                    c->tight_out, c->tight_far);
         d.seg0 = nseg;
         d.seq_off = seq_b;
         seq_b += hi;
@@ -1319,6 +1320,13 @@ int ccsx_gpu_set_tight_out(ccsx_ctx *c, uint32_t bytes)
 {
     if (!c) return -1;
     c->tight_out = bytes;
+    return 0;
+}
+
+int ccsx_gpu_set_tight_far(ccsx_ctx *c, uint32_t rows)
+{
+    if (!c) return -1;
+    c->tight_far = rows;
     return 0;
 }
 

@@ -202,9 +202,11 @@ CCSX_HD inline void zlayout(ZLayout &L, const ZmwDesc &d)
 // ~40 reads).  0: not shredded.  The output slab: S + 16 bytes bound any
 // consensus (one base per column, columns <= S); tight caps hold 2 x the
 // longest segment + 1,024 (a CCS is about one insert long; kErrOut re-runs
-// the ZMW uncapped), tight_out overriding (tests).
+// the ZMW uncapped), tight_out overriding (tests); tight_far overrides the
+// far slot records' tight row count (tests).
 CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, bool full = true,
-                          uint32_t tight_rows = 0, uint32_t shred_win = 0, uint32_t tight_out = 0)
+                          uint32_t tight_rows = 0, uint32_t shred_win = 0, uint32_t tight_out = 0,
+                          uint32_t tight_far = 0)
 {
     d.n = n;
     d.rcap = uint32_t(S + 16);
@@ -224,7 +226,7 @@ CCSX_HD inline void zcaps(ZmwDesc &d, uint64_t S, uint32_t lmax, uint32_t n, boo
     // far rows' slot records: every row (full caps), else 1 in 16 (config E
     // 0.02 %, D 0.87 % of DP rows are far); more fail the ZMW with kErrSpill
     // and it is re-run with full caps
-    d.wcap = full ? d.rcap : d.rcap / 16 + 64;
+    d.wcap = full ? d.rcap : tight_far ? tight_far : d.rcap / 16 + 64;
     d.outcap = uint32_t(S + 16);
     if (!full) {
         const uint64_t oc = tight_out ? tight_out : 2ull * lmax + 1024;

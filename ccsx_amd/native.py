@@ -23,7 +23,7 @@ MODE_PRIMITIVE = 1
 EXPORTS = {
     "ccsx_gpu.h": ["ccsx_gpu_device_count", "ccsx_gpu_open", "ccsx_gpu_close", "ccsx_gpu_error", "ccsx_gpu_status_str", "ccsx_gpu_run",
                    "ccsx_gpu_stage", "ccsx_gpu_launch", "ccsx_gpu_fetch", "ccsx_gpu_staged_bytes",
-                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows", "ccsx_gpu_set_tight_out", "ccsx_gpu_set_stage_piece",
+                   "ccsx_gpu_set_profiling", "ccsx_gpu_profile", "ccsx_gpu_profile_zmw", "ccsx_gpu_set_tight_rows", "ccsx_gpu_set_tight_out", "ccsx_gpu_set_tight_far", "ccsx_gpu_set_stage_piece",
                    "ccsx_gpu_set_mem_share", "ccsx_gpu_set_prealloc", "ccsx_gpu_set_fault",
                    "ccsx_gpu_set_kernel_cfg", "ccsx_gpu_kernel_cfg", "ccsx_gpu_rerun_count",
                    "ccsx_gpu_set_bp_log", "ccsx_gpu_bp_log", "ccsx_gpu_stage_for",
@@ -79,6 +79,8 @@ def lib() -> C.CDLL:
             L.ccsx_gpu_profile_zmw.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32]
         L.ccsx_gpu_set_tight_rows.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_tight_out.argtypes = [C.c_void_p, C.c_uint32]
+        if hasattr(L, "ccsx_gpu_set_tight_far"):  # (absent from the older builds used in A/B runs)
+            L.ccsx_gpu_set_tight_far.argtypes = [C.c_void_p, C.c_uint32]
         L.ccsx_gpu_set_stage_piece.argtypes = [C.c_void_p, C.c_uint64]
         L.ccsx_gpu_set_prealloc.argtypes = [C.c_void_p, C.c_int]
         L.ccsx_gpu_set_kernel_cfg.argtypes = [C.c_void_p, C.c_int]
@@ -478,6 +480,10 @@ class Engine:
     def set_tight_rows(self, rows: int) -> None:
         """Test hook: override the tight row capacity (0 = default)."""
         self._L.ccsx_gpu_set_tight_rows(self._ctx, rows)
+
+    def set_tight_far(self, rows: int) -> None:
+        """Test hook: override the tight far slot record rows (0 = default)."""
+        self._L.ccsx_gpu_set_tight_far(self._ctx, rows)
 
     def set_prealloc(self, on: bool) -> None:
         """Pinned staging floors and one-off slice budget, as the CLI's contexts."""

@@ -139,6 +139,10 @@ int ccsx_gpu_set_tight_rows(ccsx_ctx *ctx, uint32_t rows);
 /* Test hook: tight output slab override in bytes (0 = default 2 x longest
  * segment + 1,024; a consensus beyond it re-runs the ZMW with full caps). */
 int ccsx_gpu_set_tight_out(ccsx_ctx *ctx, uint32_t bytes);
+/* Test hook: tight far slot record rows (0 = default rcap / 16 + 64; a DP
+ * meeting more far rows -- more than four predecessors or one beyond the
+ * ring -- re-runs the ZMW with full caps, a record per row). */
+int ccsx_gpu_set_tight_far(ccsx_ctx *ctx, uint32_t rows);
 /* Test hook: half size of the piecewise subread staging (0 = 64 MiB) that a
  * preallocating context sharing its device (ccsx_gpu_set_prealloc,
  * ccsx_gpu_set_mem_share > 1: the CLI's) uses for slices larger than two

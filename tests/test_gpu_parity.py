@@ -187,6 +187,25 @@ def test_piecewise_staging():
         e.close()
 
 
+@pytest.mark.parametrize("cfg", [0, 5])
+def test_far_record_rerun(engine, cfg):
+    """Rows with more than four predecessors keep their slots in far slot
+    records of a tight capacity (rcap / 16 + 64); a DP that meets more fails
+    the ZMW with kErrSpill and ccsx_gpu_run re-runs it with full caps (a
+    record per row).  A capacity of one forces it on wide graphs (70 passes):
+    byte-equal to the oracle, on the helper and the one-wave objects."""
+    zs = [synth(6500 + h, 1500, 70) for h in range(2)]
+    engine.set_kernel_cfg(cfg)
+    engine.set_tight_far(1)
+    try:
+        before = engine.rerun_count()
+        _check(engine, zs, cx.MODE_SHRED)
+        assert engine.rerun_count() - before >= 1
+    finally:
+        engine.set_tight_far(0)
+        engine.set_kernel_cfg(-1)
+
+
 def test_tight_caps_fail_loudly_without_rerun(engine):
     """stage/launch/fetch (no re-run) reports the capacity status."""
     zs = [synth(h, 3000, 6) for h in range(2)]
