@@ -56,6 +56,11 @@ KCFGS = [(n, [f"-DCCSX_KCFG={n}", f"-DCCSX_LAUNCH=ccsx_launch_zmw_{n}", f"-DCCSX
                                    "-DCCSX_PRIO_WAVE0=0", "-DCCSX_PRIO_MERGE=0", "-DCCSX_PRIO_TB=1", "-DCCSX_PRIO_MG=1",
                                    "-DCCSX_RING16", "-DCCSX_TB_ROWS=32",
                                    "-DCCSX_WAVES_PER_EU=6"])]]
+# machine-scheduler strategy per kernel configuration (the others: max-ilp).
+# The one-wave objects under LLVM's iterative ILP scheduler, interleaved A/B
+# r08ad: E16k 541.2 -> 536.3 ms, config D 305.1 -> 302.2 ms; the latency
+# object (config B) measured +1.7 % with it and keeps max-ilp
+KSCHED: dict[str, str] = {n: "iterative-ilp" for n in ("solo", "solo16", "solo16w")}
 
 
 def _hipcc() -> str:
@@ -119,8 +124,12 @@ def build_product(verbose: bool = False) -> str:
     ]
     common = ["-O3", "-std=c++17", "-fPIC", "-I" + INC, "-I" + CSRC, "-I" + os.path.join(CSRC, "host")]
     # the kernel's per-ZMW chains are latency-bound: the ILP-maximising machine
-    # scheduler measured -0.8 % per launch on config B (tools/abn.sh)
-    kflags = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+    # scheduler measured -0.8 % per launch on config B (tools/abn.sh); per
+    # configuration, KSCHED's strategy instead (A/B in DESIGN §9)
+    def kflags_of(name: str) -> list[str]:
+        return ["-mllvm", "-amdgpu-sched-strategy=" + KSCHED.get(name, "max-ilp")]
+    # a flag change here must rebuild the kernel objects
+    khdrs = khdrs + [os.path.abspath(__file__)]
     # every object is independent: compile them concurrently (the kernel
     # objects take minutes each; host objects seconds)
     objs, jobs = [], []
@@ -130,7 +139,7 @@ def build_product(verbose: bool = False) -> str:
                 o = os.path.join(OBJ, f"ccsx_kernel_{name}.hip.o")
                 objs.append(o)
                 if _stale(o, [s] + khdrs):
-                    jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + defs + ["-c", s, "-o", o])
+                    jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags_of(name) + defs + ["-c", s, "-o", o])
             continue
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
@@ -146,7 +155,7 @@ def build_product(verbose: bool = False) -> str:
             # is not what this build measures; per-ZMW cycle counts are).  The
             # diagnostic flags come after the configuration's defines, so its
             # waves-per-EU wins over solo16's 5
-            jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags + defs
+            jobs.append([hipcc, "-x", "hip", "--offload-arch=" + ARCH] + common + kflags_of(name) + defs
                         + ["-Wno-macro-redefined", "-DCCSX_DP_STAMPS", "-DCCSX_WAVES_PER_EU=2", "-c", srcs[0], "-o", dobj])
     _run_all(jobs, verbose)
     if _stale(LIB, objs):

@@ -14,10 +14,11 @@ OBJ=$ROOT/build/obj
 # CSRC: another source tree (e.g. a git archive of an older commit) for the kernel and ccsx_gpu.cpp
 C=${CSRC:-$ROOT/ccsx_amd/csrc}
 INC="-I$ROOT/include -I$C -I$C/host"
-# KSCHED overrides the machine-scheduler flags (default: build.py's max-ilp; KSCHED=" " for LLVM's default)
-K="/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC ${KSCHED:--mllvm -amdgpu-sched-strategy=max-ilp} -Wno-macro-redefined"
+# KSCHED overrides the machine-scheduler flags (default: the configuration's strategy in
+# build.py's KSCHED, else max-ilp; KSCHED=" " for LLVM's default)
+K="/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $INC -Wno-macro-redefined"
 KOBJS=""
-while read -r NAME DEFS; do
+while read -r NAME SCHED DEFS; do
   X=("$@")
   if [ -n "$CFGS" ] && [[ " $CFGS " != *" $NAME "* ]] && [ -f $OBJ/ccsx_kernel_${NAME}.hip.o ]; then
     # a configuration outside CFGS: the product's object (also with KSRC)
@@ -26,9 +27,9 @@ while read -r NAME DEFS; do
   fi
   [ -n "$CFGS" ] && [[ " $CFGS " != *" $NAME "* ]] && X=()
   rm -f $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o
-  $K $DEFS "${X[@]}" -c ${KSRC:-$C/ccsx_kernel.hip} -o $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o &
+  $K ${KSCHED:--mllvm -amdgpu-sched-strategy=$SCHED} $DEFS "${X[@]}" -c ${KSRC:-$C/ccsx_kernel.hip} -o $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o &
   KOBJS="$KOBJS $OBJ/ccsx_kernel_${NAME}_$TAG.hip.o"
-done < <(cd "$ROOT" && python3 -c "from ccsx_amd.build import KCFGS; [print(n, ' '.join(d)) for n, d in KCFGS]")
+done < <(cd "$ROOT" && python3 -c "from ccsx_amd.build import KCFGS, KSCHED; [print(n, KSCHED.get(n, 'max-ilp'), ' '.join(d)) for n, d in KCFGS]")
 /opt/rocm/bin/hipcc -x c++ -O3 -std=c++17 -fPIC $INC -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include "$@" \
   -c $C/ccsx_gpu.cpp -o $OBJ/ccsx_gpu_$TAG.cpp.o
 wait
